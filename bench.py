@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""Swizzle encode benchmark (BASELINE.json metric: GiB/s of file bytes tagged,
+Swizzle encode, device-resident).
+
+One step = one pass of the encode hot path (hb_encode: alpha PRF + Montgomery
+conversion + the encode kernel) over every block of this rank's device-resident
+synthetic file.  Workload (BASELINE.json configs):
+  c3 (default): configs[2], 64 GiB random file, 256-bit prime, 16 sectors per
+                block -- the largest single-GPU configuration; for N > 1 every
+                rank encodes its own 64 GiB block-range shard of an N*64 GiB file
+                (weak scaling, no collective: blocks are independent).
+  c2:           configs[1], 1 GiB, 256-bit prime, 1 sector per block.
+  c4:           configs[3], 256 GiB file sharded over the N ranks (256/N GiB each).
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run, one rank per GPU (RCCL is used only for the barrier and
+the max-over-ranks time).
+
+Besides the contract fields the JSON line carries
+  roofline:     the encode kernel's algorithmic file bytes per launch / its mean
+                duration (HIP events on the kernel's stream) against the HBM
+                read peak; traffic from the rocprofv3 PMC pass when recorded in
+                profiles/ for this workload, else null; plus the LDS-lookup
+                rate, the resource that actually binds.
+  cpu_baseline: the repo's C oracle (OpenSSL AES-NI + BIGNUM, pthreads) timed on
+                this host on a bounded prefix of the same file (rank 0, N = 1).
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+P256 = int("db8709c32591ddc589b5c3c0986f92e0d11205b943c23a7e419e6c35b0256e6b", 16)
+GIB = 1 << 30
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E vendor peak (MI355X_MICROARCH.md)
+LDS_LOOKUPS_PER_CLK_CU = 32.0  # one wave-wide ds_read_b32 per 2 clocks per CU
+CLOCK_GHZ = 2.4
+NUM_CUS = 256
+
+CONFIGS = {
+    "c3": dict(name="configs[2]: 64 GiB random file, Swizzle encode, 256-bit prime, "
+                    "16 sectors/block, 1 MI355X (per rank for N>1: 64 GiB shard)",
+               gib_per_rank=64, sectors=16, weak=True),
+    "c2": dict(name="configs[1]: 1 GiB random file, Swizzle encode, 256-bit prime, "
+                    "1 sector/block (per rank for N>1)",
+               gib_per_rank=1, sectors=1, weak=True),
+    "c4": dict(name="configs[3]: 256 GiB random file, Swizzle encode, 256-bit prime, "
+                    "16 sectors/block, block ranges sharded over N GPUs",
+               gib_total=256, sectors=16, weak=False),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--gib", type=float, default=None, help="override file GiB per rank")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time the pinned/pageable host path on a 4 GiB prefix (DESIGN.md)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from heartbeat_amd import _native
+    L = _native.lib()
+    ctx = _native.context(local)
+
+    cfg = CONFIGS[args.config]
+    S = cfg["sectors"]
+    p = P256
+    pb = _native.be(p)
+    ss, w = 32, 32
+    C = ss * S
+    if args.gib is not None:
+        per_rank = int(args.gib * GIB)
+    elif cfg["weak"]:
+        per_rank = cfg["gib_per_rank"] * GIB
+    else:
+        per_rank = cfg["gib_total"] * GIB // world
+    blocks_per_rank = per_rank // C
+    global_blocks = blocks_per_rank * world + 1      # whole-file tag count (trailing empty block)
+    b0 = rank * blocks_per_rank
+    nblocks = blocks_per_rank + (1 if rank == world - 1 else 0)
+    length = blocks_per_rank * C                     # this rank's bytes
+
+    fk = hashlib.sha256(b"hb-bench-f").digest()
+    ak = hashlib.sha256(b"hb-bench-alpha").digest()
+
+    dptr = ctypes.c_void_p()
+    tptr = ctypes.c_void_p()
+    ctx.check(L.hb_device_malloc(ctx.h, length, ctypes.byref(dptr)))
+    ctx.check(L.hb_device_malloc(ctx.h, nblocks * w, ctypes.byref(tptr)))
+    # rank r's shard is bytes [b0*C, b0*C + length) of one synthetic file
+    ctx.check(L.hb_fill_random(ctx.h, dptr, length, 0x5EED0000 + 3 + rank))
+
+    tries = ctypes.c_uint64()
+
+    def step():
+        ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, b0, dptr, length, nblocks, tptr,
+                              3, ctypes.byref(tries)))
+        return ctx.last_kernel_ms()[0]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        kms.append(step())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_bytes = length * world * args.steps
+    value = total_bytes / GIB / elapsed
+    kernel_ms = sum(kms) / len(kms)
+    achieved_gbs = length / (kernel_ms * 1e-3) / 1e9
+    tries_per_block = tries.value / nblocks
+    lookups = tries.value * 32 * (16 * 12 + 5)      # nb=32 AES per try, 197 LDS lookups per AES-256
+    lds_rate = lookups / (kernel_ms * 1e-3)
+    lds_peak = NUM_CUS * CLOCK_GHZ * 1e9 * LDS_LOOKUPS_PER_CLK_CU
+
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(prof):
+        try:
+            rec = json.load(open(prof)).get(args.config)
+            if rec and rec.get("file_bytes") == length:
+                traffic = rec["hbm_bytes_per_launch"]
+        except (ValueError, KeyError):
+            traffic = None
+
+    line = {
+        "metric": "GiB/s file bytes tagged (Swizzle encode, device-resident) at 1/2/4/8 GPUs",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak" if cfg["weak"] else "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (SplitMix64 random file bytes, seeded keys)",
+        "config": {
+            "workload": cfg["name"],
+            "file_bytes_per_rank": length,
+            "blocks_total": global_blocks,
+            "sectors": S,
+            "prime_bits": 256,
+            "prime": hex(p),
+            "expected_tries_per_prf": round(2.0 ** 256 / p, 4),
+            "parallelism": "dp%d block-range shards, no collective" % world,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": "hb_encode_kernel",
+            "kernel_ms": round(kernel_ms, 3),
+            "algorithmic_bytes_per_launch": length,
+            "binding_resource": {
+                "resource": "LDS ds_read_b32 T-table lookups",
+                "achieved_per_s": lds_rate,
+                "peak_per_s": lds_peak,
+                "frac": round(lds_rate / lds_peak, 4),
+            },
+        },
+        "prf_tries_per_block": round(tries_per_block, 4),
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C,
+                                            args.cpu_seconds, args.cpu_threads)
+    if rank == 0 and args.host_path:
+        line["host_path"] = host_path(ctx, L, dptr, length, S, pb, fk, ak, C)
+
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.check(L.hb_device_free(ctx.h, dptr))
+    ctx.check(L.hb_device_free(ctx.h, tptr))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads):
+    """Oracle (kind "port") on successive 256 MiB prefixes of the same file
+    until `seconds` of CPU work, on `threads` host threads."""
+    import numpy as np
+    from oracle import oracle as O
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    piece = (256 << 20) // C * C
+    host = np.empty(piece, dtype=np.uint8)
+    out = np.empty((piece // C) * 32, dtype=np.uint8)
+    done = 0
+    busy = 0.0
+    off = 0
+    while busy < seconds and off < length:
+        n = min(piece, length - off)
+        ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value + off, n, 2))
+        nb = n // C
+        t = time.perf_counter()
+        rc = O.encode_raw(p, S, fk, ak, host.ctypes.data, n, off // C, nb, out.ctypes.data, threads)
+        busy += time.perf_counter() - t
+        if rc:
+            raise RuntimeError("oracle error %d" % rc)
+        done += n
+        off += n
+    return {"value": round(done / GIB / busy, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d MiB prefix of the same synthetic file (%d blocks), oracle/swizzle_oracle.c "
+                      "(OpenSSL AES-NI CFB8 + BIGNUM), %d pthreads, %.1f s" % (
+                          done >> 20, done // C, threads, busy)}
+
+
+def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
+    """Rate with the file in (pageable) host memory: chunked H2D + encode + D2H tags."""
+    import numpy as np
+    n = min(length, 4 * GIB) // C * C
+    host = np.empty(n, dtype=np.uint8)
+    ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value, n, 2))
+    nb = n // C
+    tags = np.empty(nb * 32, dtype=np.uint8)
+    t = time.perf_counter()
+    ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, host.ctypes.data, n, nb,
+                          tags.ctypes.data, 0, None))
+    dt = time.perf_counter() - t
+    return {"value": round(n / GIB / dt, 3), "unit": "GiB/s", "bytes": n,
+            "note": "pageable host buffer, 256 MiB chunks, H2D overlapped with encode"}
+
+
+if __name__ == "__main__":
+    main()

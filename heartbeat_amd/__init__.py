@@ -1,0 +1,18 @@
+"""heartbeat_amd -- MI355X-native Swizzle (Shacham-Waters private PDP)
+encode/prove hot path behind the heartbeat API.
+
+    import heartbeat_amd.PySwizzle as PySwizzle     # drop-in for heartbeat.PySwizzle
+    from heartbeat_amd import HeartbeatError
+
+Compute runs in hand-written HIP kernels for gfx950 (libhbswizzle.so, C ABI in
+include/hbswizzle.h); see DESIGN.md.  The C++ ``heartbeat.Swizzle`` object and
+the Merkle / OneHash schemes are outside this build's scope, so
+``Heartbeat`` is the PySwizzle scheme here.
+"""
+__version__ = "0.1.4"
+
+from . import PySwizzle  # NOQA
+from .exc import HeartbeatError  # NOQA
+from .util import KeyedPRF  # NOQA
+
+Heartbeat = PySwizzle.PySwizzle

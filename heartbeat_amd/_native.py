@@ -1,0 +1,144 @@
+"""ctypes binding of libhbswizzle.so (C ABI: include/hbswizzle.h).
+
+The library must have been built (``heartbeat_amd.build.build()`` or
+``python __graft_entry__.py``); importing the compute entry points without it,
+or calling them without a usable gfx950 GPU, raises HeartbeatError.  There is
+no CPU fallback for encode / prove / verify / KeyedPRF.
+"""
+import ctypes
+import os
+import threading
+
+from .exc import HeartbeatError
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhbswizzle.so")
+
+HB_DATA_ON_DEVICE = 1
+HB_TAGS_ON_DEVICE = 2
+
+_lib = None
+_lib_lock = threading.Lock()
+_ctxs = {}
+
+# (name, restype, argtypes) for every symbol of include/hbswizzle.h
+_c = ctypes
+_P = _c.c_void_p
+_B = _c.c_char_p
+SIGNATURES = [
+    ("hb_abi_version", _c.c_int, []),
+    ("hb_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_P)]),
+    ("hb_ctx_destroy", None, [_P]),
+    ("hb_last_error", _c.c_char_p, [_P]),
+    ("hb_width", _c.c_size_t, [_B, _c.c_size_t]),
+    ("hb_prf_eval", _c.c_int, [_P, _B, _c.c_size_t, _B, _c.c_size_t, _P, _c.c_size_t, _P]),
+    ("hb_encode", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _B, _c.c_size_t, _c.c_uint64,
+                             _P, _c.c_uint64, _c.c_uint64, _P, _c.c_uint32,
+                             _c.POINTER(_c.c_uint64)]),
+    ("hb_block_count", _c.c_uint64, [_B, _c.c_size_t, _c.c_uint32, _c.c_uint64]),
+    ("hb_prove", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _c.c_size_t, _c.c_uint64, _B,
+                            _c.c_size_t, _P, _c.c_uint64, _P, _c.c_uint64, _c.c_uint32, _P, _P]),
+    ("hb_verify_rhs", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _B, _c.c_size_t,
+                                 _c.c_uint64, _B, _c.c_size_t, _c.c_uint64, _B, _c.c_size_t,
+                                 _B, _P]),
+    ("hb_aes_cfb8", _c.c_int, [_B, _c.c_size_t, _B, _B, _P, _c.c_size_t, _c.c_int]),
+    ("hb_last_kernel_ms", _c.c_int, [_P, _c.POINTER(_c.c_double), _c.POINTER(_c.c_uint32)]),
+    ("hb_device_malloc", _c.c_int, [_P, _c.c_uint64, _c.POINTER(_P)]),
+    ("hb_device_free", _c.c_int, [_P, _P]),
+    ("hb_memcpy", _c.c_int, [_P, _P, _P, _c.c_uint64, _c.c_int]),
+    ("hb_fill_random", _c.c_int, [_P, _P, _c.c_uint64, _c.c_uint64]),
+]
+
+
+def lib():
+    """The loaded library (raises HeartbeatError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HeartbeatError(
+                    "libhbswizzle.so is not built (%s); run heartbeat_amd.build.build()" % LIB_PATH)
+            L = ctypes.CDLL(LIB_PATH)
+            for name, res, args in SIGNATURES:
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+    return _lib
+
+
+def default_device():
+    for var in ("HB_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(var, "").strip():
+            return int(os.environ[var])
+    return 0
+
+
+class Context(object):
+    """One libhbswizzle context (stream + scratch) on one GPU."""
+
+    def __init__(self, device):
+        L = lib()
+        h = ctypes.c_void_p()
+        rc = L.hb_ctx_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise HeartbeatError("cannot open GPU %d: %s" % (
+                device, L.hb_last_error(None).decode("utf-8", "replace")))
+        self.h = h
+        self.device = int(device)
+        self.lock = threading.Lock()
+
+    def check(self, rc):
+        if rc != 0:
+            raise HeartbeatError(lib().hb_last_error(self.h).decode("utf-8", "replace"))
+
+    def last_kernel_ms(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_uint32()
+        lib().hb_last_kernel_ms(self.h, ctypes.byref(ms), ctypes.byref(n))
+        return ms.value, n.value
+
+    def close(self):
+        if self.h:
+            lib().hb_ctx_destroy(self.h)
+            self.h = None
+
+
+def context(device=None):
+    """The process-wide context for `device` (default: $HB_DEVICE, $LOCAL_RANK or 0)."""
+    d = default_device() if device is None else int(device)
+    c = _ctxs.get(d)
+    if c is None:
+        with _lib_lock:
+            c = _ctxs.get(d)
+            if c is None:
+                c = Context(d)
+                _ctxs[d] = c
+    return c
+
+
+def be(n, width=None):
+    n = int(n)
+    if width is None:
+        width = max(1, (n.bit_length() + 7) // 8)
+    return n.to_bytes(width, "big")
+
+
+def width_of(p):
+    return (int(p).bit_length() + 7) // 8
+
+
+def aes_cfb8(key, iv, data, encrypt):
+    """Host AES-CFB8 (State encryption, PySwizzle.py:162-195)."""
+    key = bytes(key)
+    iv = bytes(iv)
+    data = bytes(data)
+    if len(iv) != 16:
+        raise HeartbeatError("IV must be 16 bytes long")
+    out = ctypes.create_string_buffer(max(1, len(data)))
+    rc = lib().hb_aes_cfb8(key, len(key), iv, data, out, len(data), 1 if encrypt else 0)
+    if rc != 0:
+        raise HeartbeatError("AES key must be either 16, 24, or 32 bytes long")
+    return out.raw[:len(data)]

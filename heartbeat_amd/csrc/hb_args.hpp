@@ -1,0 +1,80 @@
+// hb_args.hpp -- kernel argument blocks shared by hb_kernels.hip and the host
+// runtime (hb_runtime.cpp).  All passed by value (kernarg segment), so the
+// round keys, modulus and range are wave-uniform scalar operands.
+#pragma once
+#include "hb_lane.hpp"
+
+// Workgroup geometry of the PRF engine kernels: 512 threads (8 waves) and a
+// 64 KiB LDS T-table image per workgroup -> 2 workgroups (16 waves) per CU.
+#define HB_ENGINE_WG 512
+#define HB_QUEUE_CHUNK 256
+// PRF tries after which a job is abandoned and reported (see hb_engine)
+#define HB_MAX_TRIES 2048u
+// job-queue counters per slot: [0] next job, [1] PRF tries, [2] abandoned jobs
+#define HB_QSLOT 4
+
+template <int NL>
+struct EncodeArgs {
+    PrfParams<NL> prf;            // F = KeyedPRF(f_key, p)
+    ModP<NL> mod;
+    const unsigned char *data;    // block k of this launch starts at data[k*C]
+    u64 len;                      // bytes of `data` (end of file)
+    u64 nblocks;
+    u64 block_base;               // global index of block 0 (PRF input)
+    unsigned char *tags;          // nblocks * tw big-endian bytes
+    const u32 *alpha_mont;        // S * NL limbs: alpha_j R mod p
+    const u32 *t0;                // 256-entry T0 table (global)
+    unsigned long long *queue;    // HB_QSLOT counters, see above
+    u64 C;
+    u32 tw, ss, S, pad_;
+};
+
+template <int NL>
+struct PrfArgs {
+    PrfParams<NL> prf;
+    const u64 *xs;                // inputs (device) or nullptr: x = x0 + k
+    u64 x0;
+    u64 n;
+    u32 *out;                     // n * NL little-endian limbs
+    const u32 *t0;
+    unsigned long long *queue;
+};
+
+template <int NL>
+struct MontArgs {
+    ModP<NL> mod;
+    u32 r2[NL];                   // R^2 mod p
+    const u32 *in;                // n * NL limbs, each < R
+    u32 *out;                     // n * NL limbs: in * R mod p
+    u64 n;
+};
+
+// Weighted sums  sum_i w_i * value_{col}(i)  mod p  (w_i in Montgomery form).
+//   mode 0 (prove, device-resident file):  col < S -> sector col of block idx[i]
+//           of data; col == S -> tag idx[i] (tw big-endian bytes)
+//   mode 1 (verify): single column, value = vals[i] (NL limbs)
+//   mode 2 (prove, host-gathered blocks):  as mode 0 with block i of the
+//           gathered buffer (blen[i] valid bytes) and gathered tag i
+template <int NL>
+struct WsumArgs {
+    ModP<NL> mod;
+    u32 mode, ncols;
+    const u64 *idx;
+    const u32 *w;
+    u64 nterms;
+    const unsigned char *data;
+    u64 len, C;
+    u32 ss, S, tw, pad_;
+    const unsigned char *tags;
+    const u32 *vals;
+    const u64 *blen;
+    u32 *partials;                // [ncols][nthreads][NL]
+};
+
+template <int NL>
+struct SumArgs {
+    ModP<NL> mod;
+    const u32 *partials;          // [ncols][nparts][NL], each < p
+    u32 nparts;
+    u32 *out;                     // [ncols][NL]
+};

@@ -1,0 +1,372 @@
+// hb_kernels.hip -- CDNA4 (gfx950) kernels of the Swizzle hot path.
+//
+//   hb_encode_kernel   tags of a run of blocks     (PySwizzle.py:296-309)
+//   hb_prf_kernel      batched KeyedPRF.eval        (util.py:83-96)
+//   hb_mont_kernel     x -> x R mod p (Montgomery form of alpha_j, v_i)
+//   hb_wsum_kernel     per-thread partial sums of w_i * value(i) for prove /
+//                      verify (PySwizzle.py:351-368, :388-394)
+//   hb_sum_kernel      mod-p tree reduction of the partials
+//   hb_fill_kernel     synthetic file bytes (SplitMix64), benches and tests
+//
+// PRF engine.  KeyedPRF.eval is rejection sampling (E[tries] = 2^bitlen(R)/R,
+// up to 2): a lane-per-block loop where each lane retries until accepted would
+// run every wave for the MAX of 64 geometric trip counts (~3x the mean).
+// Instead each lane owns a job (block / PRF input) and the wave re-deals jobs
+// after every try: lanes whose try was accepted finish their job and take the
+// next ones from a wave-local pool refilled from a global counter
+// (HB_QUEUE_CHUNK jobs per atomic).  Every try of every lane is useful work
+// until the queue drains.  One try = nb CFB-8 steps = nb AES encryptions of
+// which only byte 0 is used (hb_lane.hpp).
+//
+// The AES T tables live in LDS as a 64 KiB bank-replicated T0/T1 image
+// (hb_lane.hpp, LaneTab): ds_read_b32 lookups are conflict-free for any
+// indices, and the per-CU LDS rate (one wave-wide ds_read_b32 per 2 cycles)
+// is the kernel's binding resource (roofline).
+#include <hip/hip_runtime.h>
+#include "hb_args.hpp"
+
+#define HB_LDS_WORDS (HB_TAB_BYTES / 4)
+
+// Expand the 256-entry global T0 into the replicated LDS image.
+__device__ __forceinline__ void hb_fill_lds(u32 *lds, const u32 *t0) {
+    // 16-byte writes: word group g covers words 4g..4g+3 = same (entry, table)
+    for (u32 g = threadIdx.x; g < HB_LDS_WORDS / 4; g += blockDim.x) {
+        const u32 e = g >> 4, t = (g >> 3) & 1u;
+        u32 v = t0[e];
+        if (t) v = (v << 8) | (v >> 24);
+        reinterpret_cast<uint4 *>(lds)[g] = make_uint4(v, v, v, v);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ u32 hb_lane_id() { return threadIdx.x & 63u; }
+
+__device__ __forceinline__ u32 hb_mbcnt(u64 mask) {
+    return __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
+}
+
+__device__ __forceinline__ u64 hb_bcast64(u64 v) {
+    u32 lo = __builtin_amdgcn_readfirstlane((u32)v);
+    u32 hi = __builtin_amdgcn_readfirstlane((u32)(v >> 32));
+    return ((u64)hi << 32) | lo;
+}
+
+// Wave-local job pool over a global counter.  All members are wave-uniform.
+struct HbPool {
+    u64 next, end, njobs;
+    unsigned long long *counter;
+    bool exhausted;
+
+    // Lanes in `mask` (wave-uniform ballot) each want one job; returns whether
+    // this lane (if `want`) got one, in `job`.
+    __device__ __forceinline__ bool take(u64 mask, bool want, u64 &job) {
+        const u32 need = (u32)__popcll(mask);
+        const u32 rank = hb_mbcnt(mask);
+        const u64 avail = end - next;
+        u64 base2 = 0, got2 = 0;
+        if (avail < need && !exhausted) {
+            u64 b = 0;
+            if (hb_lane_id() == 0) b = atomicAdd(counter, (unsigned long long)HB_QUEUE_CHUNK);
+            b = hb_bcast64(b);
+            if (b >= njobs) {
+                exhausted = true;
+            } else {
+                base2 = b;
+                got2 = njobs - b < (u64)HB_QUEUE_CHUNK ? njobs - b : (u64)HB_QUEUE_CHUNK;
+            }
+        }
+        bool ok = false;
+        if (want) {
+            if ((u64)rank < avail) {
+                job = next + rank;
+                ok = true;
+            } else if ((u64)rank - avail < got2) {
+                job = base2 + ((u64)rank - avail);
+                ok = true;
+            }
+        }
+        if ((u64)need <= avail) {
+            next += need;
+        } else {
+            const u64 used2 = (u64)need - avail < got2 ? (u64)need - avail : got2;
+            next = base2 + used2;
+            end = base2 + got2;
+        }
+        return ok;
+    }
+};
+
+// The PRF engine: runs KeyedPRF.eval for every job of the queue and calls
+// h.accept(job, value) once per job with the accepted value.
+template <int NL, int NR, class H>
+__device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParams<NL> &P,
+                                          u64 njobs, unsigned long long *queue) {
+    HbPool pool{0, 0, njobs, queue, false};
+    u64 job = 0;
+    bool active = pool.take(__ballot(1), true, job);
+    u32 dig[8], sr[4] = {0, 0, 0, 0}, out[NL];
+    if (active) hb_sha256_decimal(h.x_of(job), dig);
+    u32 tries = 0, job_tries = 0, failed = 0;
+    while (__ballot(active)) {
+        const u32 ok = hb_prf_try<NL, NR>(L, P, sr, dig, out);
+        tries += active ? 1u : 0u;
+        job_tries += 1u;
+        const bool acc = active && ok;
+        if (acc) h.accept(job, out);
+        // Exit guarantee: a job still rejected after HB_MAX_TRIES tries
+        // (probability <= 2^-HB_MAX_TRIES for any valid range) is dropped and
+        // counted in queue[2]; the host reports it as an error.
+        const bool give_up = active && !ok && job_tries >= HB_MAX_TRIES;
+        failed += give_up ? 1u : 0u;
+        const bool next = acc || give_up;
+        const u64 m = __ballot(next);
+        if (m) {
+            u64 nj = 0;
+            const bool got = pool.take(m, next, nj);
+            if (next) {
+                active = got;
+                job = nj;
+                job_tries = 0;
+                sr[0] = sr[1] = sr[2] = sr[3] = 0;   // fresh cipher per eval (util.py:88)
+                if (got) hb_sha256_decimal(h.x_of(job), dig);
+            }
+        }
+    }
+    // statistics: one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        tries += __shfl_xor(tries, off);
+        failed += __shfl_xor(failed, off);
+    }
+    if (hb_lane_id() == 0 && tries) atomicAdd(queue + 1, (unsigned long long)tries);
+    if (hb_lane_id() == 0 && failed) atomicAdd(queue + 2, (unsigned long long)failed);
+}
+
+// ------------------------------------------------------------------ encode
+template <int NL, int ALIGN>
+struct EncodeHandler {
+    const EncodeArgs<NL> &A;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return A.block_base + job; }
+    __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
+        u32 tag[NL];
+        hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
+        hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, tag);
+    }
+};
+
+template <int NL, int NR, int ALIGN>
+__global__ __launch_bounds__(HB_ENGINE_WG) void hb_encode_kernel(EncodeArgs<NL> A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L{(const char *)lds, (threadIdx.x & 31u) * 4u, 128u + (threadIdx.x & 31u) * 4u};
+    EncodeHandler<NL, ALIGN> h{A};
+    hb_engine<NL, NR>(h, L, A.prf, A.nblocks, A.queue);
+}
+
+// ------------------------------------------------------------------ PRF batch
+template <int NL>
+struct PrfHandler {
+    const PrfArgs<NL> &A;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return A.xs ? A.xs[job] : A.x0 + job; }
+    __device__ __forceinline__ void accept(u64 job, const u32 v[NL]) const {
+        u32 *o = A.out + job * NL;
+        for (int t = 0; t < NL; ++t) o[t] = v[t];
+    }
+};
+
+template <int NL, int NR>
+__global__ __launch_bounds__(HB_ENGINE_WG) void hb_prf_kernel(PrfArgs<NL> A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L{(const char *)lds, (threadIdx.x & 31u) * 4u, 128u + (threadIdx.x & 31u) * 4u};
+    PrfHandler<NL> h{A};
+    hb_engine<NL, NR>(h, L, A.prf, A.n, A.queue);
+}
+
+// ------------------------------------------------------------------ Montgomery
+template <int NL>
+__global__ __launch_bounds__(256) void hb_mont_kernel(MontArgs<NL> A) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    u32 x[NL], y[NL];
+    for (int t = 0; t < NL; ++t) x[t] = A.in[i * NL + t];
+    hb_to_mont<NL>(x, A.r2, A.mod, y);
+    for (int t = 0; t < NL; ++t) A.out[i * NL + t] = y[t];
+}
+
+// ------------------------------------------------------------------ prove / verify sums
+template <int NL, int ALIGN>
+__device__ __forceinline__ void hb_sector_value(const unsigned char *data, u64 len, u64 pos,
+                                                u32 ss, u32 m[NL]) {
+    if (pos >= len) {
+        for (int t = 0; t < NL; ++t) m[t] = 0;
+    } else if (pos + ss <= len) {
+        if (ALIGN == 16) hb_load_be_16<NL>(data, pos, ss, m);
+        else hb_load_be_bytes<NL>(data, pos, ss, m);
+    } else {
+        hb_load_be_bytes<NL>(data, pos, (u32)(len - pos), m);
+    }
+}
+
+template <int NL, int ALIGN>
+__global__ __launch_bounds__(256) void hb_wsum_kernel(WsumArgs<NL> A) {
+    const u32 col = blockIdx.y;
+    const u64 tid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 nthreads = (u64)gridDim.x * blockDim.x;
+    u32 acc[2 * NL + 1];
+    for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
+    u32 m[NL];
+    for (u64 i = tid; i < A.nterms; i += nthreads) {
+        if (A.mode == 1) {
+            for (int t = 0; t < NL; ++t) m[t] = A.vals[i * NL + t];
+        } else {
+            const bool gathered = A.mode == 2;
+            const u64 blk = gathered ? i : A.idx[i];
+            if (col < A.S) {
+                const u64 blen = gathered ? A.blen[i] : A.len;
+                const u64 base = gathered ? i * A.C : blk * A.C;
+                const u64 pos = base + (u64)col * A.ss;
+                const u64 end = gathered ? base + blen : A.len;
+                hb_sector_value<NL, ALIGN>(A.data, end, pos, A.ss, m);
+            } else {
+                hb_load_be_bytes<NL>(A.tags, blk * A.tw, A.tw, m);
+            }
+        }
+        hb_mac<NL>(acc, A.w + i * NL, m);
+    }
+    u32 v[NL + 1], r[NL];
+    hb_redc<NL>(acc, A.mod, v);
+    hb_reduce_small<NL>(v, A.mod, r);
+    u32 *o = A.partials + ((u64)col * nthreads + tid) * NL;
+    for (int t = 0; t < NL; ++t) o[t] = r[t];
+}
+
+// one workgroup per column: sum nparts residues mod p
+template <int NL>
+__global__ __launch_bounds__(256) void hb_sum_kernel(SumArgs<NL> A) {
+    __shared__ u32 sh[256 * NL];
+    const u32 col = blockIdx.x;
+    u32 v[NL + 1];
+    for (int t = 0; t <= NL; ++t) v[t] = 0;
+    for (u32 k = threadIdx.x; k < A.nparts; k += blockDim.x) {
+        const u32 *x = A.partials + ((u64)col * A.nparts + k) * NL;
+        u64 c = 0;
+        for (int t = 0; t < NL; ++t) {
+            c += (u64)v[t] + x[t];
+            v[t] = (u32)c;
+            c >>= 32;
+        }
+        v[NL] += (u32)c;
+    }
+    u32 r[NL];
+    hb_reduce_small<NL>(v, A.mod, r);
+    for (int t = 0; t < NL; ++t) sh[threadIdx.x * NL + t] = r[t];
+    __syncthreads();
+    for (u32 s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            u32 w[NL + 1];
+            u64 c = 0;
+            for (int t = 0; t < NL; ++t) {
+                c += (u64)sh[threadIdx.x * NL + t] + sh[(threadIdx.x + s) * NL + t];
+                w[t] = (u32)c;
+                c >>= 32;
+            }
+            w[NL] = (u32)c;
+            hb_reduce_small<NL>(w, A.mod, r);
+            for (int t = 0; t < NL; ++t) sh[threadIdx.x * NL + t] = r[t];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < NL) A.out[col * NL + threadIdx.x] = sh[threadIdx.x];
+}
+
+// ------------------------------------------------------------------ synthetic data
+__device__ __forceinline__ u64 hb_splitmix(u64 x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// byte k of the stream = byte (k & 7) (little-endian) of splitmix(seed ^ (k >> 3) * golden)
+__global__ __launch_bounds__(256) void hb_fill_kernel(unsigned char *dst, u64 len, u64 seed) {
+    const u64 nthreads = (u64)gridDim.x * blockDim.x;
+    for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q * 16 < len; q += nthreads) {
+        const u64 a = hb_splitmix(seed ^ ((2 * q) * 0xD1B54A32D192ED03ull));
+        const u64 b = hb_splitmix(seed ^ ((2 * q + 1) * 0xD1B54A32D192ED03ull));
+        if (q * 16 + 16 <= len) {
+            *reinterpret_cast<uint4 *>(dst + q * 16) =
+                make_uint4((u32)a, (u32)(a >> 32), (u32)b, (u32)(b >> 32));
+        } else {
+            for (u64 k = q * 16; k < len; ++k) {
+                const u64 w = (k - q * 16) < 8 ? a : b;
+                dst[k] = (unsigned char)(w >> (8 * ((k - q * 16) & 7)));
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+// Plain C++ entry points for hb_runtime.cpp (explicit instantiation per
+// limb count NL, AES rounds NR and sector alignment class).
+template <int NL>
+hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int grid, hipStream_t s) {
+    dim3 g(grid), b(HB_ENGINE_WG);
+#define HB_ENC(NRV, AL) hipLaunchKernelGGL((hb_encode_kernel<NL, NRV, AL>), g, b, 0, s, A)
+    if (align == 16) {
+        if (nr == 14) HB_ENC(14, 16); else if (nr == 12) HB_ENC(12, 16); else HB_ENC(10, 16);
+    } else {
+        if (nr == 14) HB_ENC(14, 1); else if (nr == 12) HB_ENC(12, 1); else HB_ENC(10, 1);
+    }
+#undef HB_ENC
+    return hipGetLastError();
+}
+
+template <int NL>
+hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int grid, hipStream_t s) {
+    dim3 g(grid), b(HB_ENGINE_WG);
+    if (nr == 14) hipLaunchKernelGGL((hb_prf_kernel<NL, 14>), g, b, 0, s, A);
+    else if (nr == 12) hipLaunchKernelGGL((hb_prf_kernel<NL, 12>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((hb_prf_kernel<NL, 10>), g, b, 0, s, A);
+    return hipGetLastError();
+}
+
+template <int NL>
+hipError_t hb_launch_mont(const MontArgs<NL> &A, hipStream_t s) {
+    const u64 grid = (A.n + 255) / 256;
+    hipLaunchKernelGGL((hb_mont_kernel<NL>), dim3((u32)grid), dim3(256), 0, s, A);
+    return hipGetLastError();
+}
+
+template <int NL>
+hipError_t hb_launch_wsum(const WsumArgs<NL> &A, int align, int gridx, hipStream_t s) {
+    dim3 g(gridx, A.ncols), b(256);
+    if (align == 16) hipLaunchKernelGGL((hb_wsum_kernel<NL, 16>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((hb_wsum_kernel<NL, 1>), g, b, 0, s, A);
+    return hipGetLastError();
+}
+
+template <int NL>
+hipError_t hb_launch_sum(const SumArgs<NL> &A, int ncols, hipStream_t s) {
+    hipLaunchKernelGGL((hb_sum_kernel<NL>), dim3(ncols), dim3(256), 0, s, A);
+    return hipGetLastError();
+}
+
+hipError_t hb_launch_fill(unsigned char *dst, u64 len, u64 seed, hipStream_t s) {
+    u64 q = (len + 15) / 16;
+    u64 grid = (q + 255) / 256;
+    if (grid > 65536) grid = 65536;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(hb_fill_kernel, dim3((u32)grid), dim3(256), 0, s, dst, len, seed);
+    return hipGetLastError();
+}
+
+#define HB_INST(NL)                                                                              \
+    template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, hipStream_t); \
+    template hipError_t hb_launch_prf<NL>(const PrfArgs<NL> &, int, int, hipStream_t);           \
+    template hipError_t hb_launch_mont<NL>(const MontArgs<NL> &, hipStream_t);                   \
+    template hipError_t hb_launch_wsum<NL>(const WsumArgs<NL> &, int, int, hipStream_t);         \
+    template hipError_t hb_launch_sum<NL>(const SumArgs<NL> &, int, hipStream_t);
+HB_INST(8)
+HB_INST(16)
+HB_INST(32)
+template hipError_t hb_launch_prf<2>(const PrfArgs<2> &, int, int, hipStream_t);

@@ -1,0 +1,461 @@
+// hb_lane.hpp -- per-lane arithmetic of the Swizzle hot path.
+//
+// Everything a single lane does for one block lives here:
+//   * SHA-256 of the decimal block index          (heartbeat/util.py:91)
+//   * AES-CFB8 keystream with byte-0-only output   (heartbeat/util.py:88-93)
+//     using a bank-replicated T0/T1 LDS image
+//   * the rejection test num < R                    (heartbeat/util.py:94)
+//   * the fixed-width Montgomery multiply-accumulate and reduction of
+//     tag = F(i) + sum_j alpha_j m_ij mod p        (PySwizzle.py:297-307)
+//
+// The header compiles as HIP device code (inlined into the kernels of
+// hb_kernels.hip) and as plain C++ (tests/emul), so the lane logic can be
+// checked against the CPU oracle without a GPU.  Wave-level work distribution
+// (job queue, ballots) is in hb_kernels.hip, not here.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIP__)
+#define HB_HD __device__ __forceinline__
+#else
+#define HB_HD static inline
+#endif
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+// ------------------------------------------------------------------ intrinsics
+HB_HD u32 hb_perm(u32 s0, u32 s1, u32 sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(s0, s1, sel);
+#else
+    // v_perm_b32: selector byte b picks byte b of {s0:s1} (0-3 = s1, 4-7 = s0),
+    // 12 = 0x00, >= 13 = 0xff (8-11, sign replication, unused here).
+    u64 v = ((u64)s0 << 32) | s1;
+    u32 r = 0;
+    for (int i = 0; i < 4; ++i) {
+        u32 b = (sel >> (8 * i)) & 0xffu, o;
+        if (b < 8) o = (u32)(v >> (8 * b)) & 0xffu;
+        else if (b == 12) o = 0;
+        else o = 0xffu;
+        r |= o << (8 * i);
+    }
+    return r;
+#endif
+}
+
+// ({hi,lo} >> sh)[31:0], sh in [0,31]
+HB_HD u32 hb_alignbit(u32 hi, u32 lo, u32 sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+    return (u32)((((u64)hi << 32) | lo) >> (sh & 31));
+#endif
+}
+
+HB_HD u32 hb_rotl16(u32 x) { return hb_alignbit(x, x, 16); }
+HB_HD u32 hb_bswap(u32 x) { return hb_perm(x, x, 0x00010203u); }
+
+// ------------------------------------------------------------------ AES
+// LDS image of the T tables, 64 KiB: entry e of table t (t = 0: T0, 1: T1 =
+// rotl8(T0)) replica r (0..31) is the u32 at byte
+//     e*256 + t*128 + r*4.
+// Lane l reads replica (l & 31), so the 32 lanes of each ds_read_b32 half-wave
+// hit 32 distinct banks (bank = (addr/4) mod 32) whatever the indices: no bank
+// conflicts.  The address of T_t[byte k of x] is one v_perm:
+//     {0, 0, x.byte[k], lb_t},  lb_t = t*128 + (lane&31)*4.
+// T2 = rotl16(T0), T3 = rotl16(T1) are applied to the XOR of the T0/T1 pair.
+#define HB_TAB_BYTES 65536
+
+struct LaneTab {
+    const char *tab;   // LDS image base (generic pointer; LDS after inlining)
+    u32 lb0, lb1;      // lane bases for T0 and T1
+};
+
+HB_HD u32 hb_tab_ld(const char *tab, u32 addr) {
+    return *(const u32 *)(tab + addr);
+}
+
+template <int K>
+HB_HD u32 hb_t(const LaneTab &L, u32 x, u32 lb) {
+    u32 addr = hb_perm(x, lb, 0x0c0c0000u | ((4u + K) << 8));
+    return hb_tab_ld(L.tab, addr);
+}
+
+// One full AES round on little-endian column words (byte r of w_c = row r).
+HB_HD void hb_aes_round(const LaneTab &L, const u32 *rk, u32 &w0, u32 &w1, u32 &w2, u32 &w3) {
+    u32 a0 = hb_t<0>(L, w0, L.lb0), b0 = hb_t<1>(L, w1, L.lb1);
+    u32 c0 = hb_t<2>(L, w2, L.lb0), d0 = hb_t<3>(L, w3, L.lb1);
+    u32 a1 = hb_t<0>(L, w1, L.lb0), b1 = hb_t<1>(L, w2, L.lb1);
+    u32 c1 = hb_t<2>(L, w3, L.lb0), d1 = hb_t<3>(L, w0, L.lb1);
+    u32 a2 = hb_t<0>(L, w2, L.lb0), b2 = hb_t<1>(L, w3, L.lb1);
+    u32 c2 = hb_t<2>(L, w0, L.lb0), d2 = hb_t<3>(L, w1, L.lb1);
+    u32 a3 = hb_t<0>(L, w3, L.lb0), b3 = hb_t<1>(L, w0, L.lb1);
+    u32 c3 = hb_t<2>(L, w1, L.lb0), d3 = hb_t<3>(L, w2, L.lb1);
+    w0 = a0 ^ b0 ^ rk[0] ^ hb_rotl16(c0 ^ d0);
+    w1 = a1 ^ b1 ^ rk[1] ^ hb_rotl16(c1 ^ d1);
+    w2 = a2 ^ b2 ^ rk[2] ^ hb_rotl16(c2 ^ d2);
+    w3 = a3 ^ b3 ^ rk[3] ^ hb_rotl16(c3 ^ d3);
+}
+
+// Byte 0 of AES_k(state).  CFB-8 consumes only that byte, so round NR-1
+// computes one byte of column 0 (4 lookups) and the last round one S-box
+// lookup (S[x] = byte 1 of T0[x]): 16*(NR-2) + 5 lookups per block.
+template <int NR>
+HB_HD u32 hb_aes_byte0(const LaneTab &L, const u32 *rk, u32 s0, u32 s1, u32 s2, u32 s3) {
+    u32 w0 = s0 ^ rk[0], w1 = s1 ^ rk[1], w2 = s2 ^ rk[2], w3 = s3 ^ rk[3];
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int r = 1; r <= NR - 2; ++r) hb_aes_round(L, rk + 4 * r, w0, w1, w2, w3);
+    u32 a = hb_t<0>(L, w0, L.lb0), b = hb_t<1>(L, w1, L.lb1);
+    u32 c = hb_t<2>(L, w2, L.lb0), d = hb_t<3>(L, w3, L.lb1);
+    u32 t = a ^ b ^ rk[4 * (NR - 1)];
+    u32 s = (t ^ ((c ^ d) >> 16)) & 0xffu;
+    u32 o = hb_t<0>(L, s, L.lb0) >> 8;
+    return (o ^ rk[4 * NR]) & 0xffu;
+}
+
+// ------------------------------------------------------------------ SHA-256
+HB_HD u32 hb_rotr(u32 x, u32 n) { return hb_alignbit(x, x, n); }
+
+// SHA-256 of ASCII decimal(x) (str(x).encode(), util.py:91); one compression
+// since len <= 20 < 56.  Digest as 8 big-endian words.
+HB_HD void hb_sha256_decimal(u64 x, u32 H[8]) {
+    // Build the message right-to-left: shifting a 24-byte big-endian register
+    // right by one byte per digit and inserting the digit at the top leaves
+    // the decimal string left-aligned with the 0x80 pad byte right behind it.
+    u32 R0 = 0x80000000u, R1 = 0, R2 = 0, R3 = 0, R4 = 0, R5 = 0;
+    u32 n = 0;
+    do {
+        u64 q = x / 10u;
+        u32 dgt = (u32)(x - q * 10u);
+        x = q;
+        R5 = hb_alignbit(R4, R5, 8);
+        R4 = hb_alignbit(R3, R4, 8);
+        R3 = hb_alignbit(R2, R3, 8);
+        R2 = hb_alignbit(R1, R2, 8);
+        R1 = hb_alignbit(R0, R1, 8);
+        R0 = (R0 >> 8) | ((0x30u + dgt) << 24);
+        ++n;
+    } while (x != 0);
+    u32 W[16] = {R0, R1, R2, R3, R4, R5, 0, 0, 0, 0, 0, 0, 0, 0, 0, n * 8u};
+    const u32 K[64] = {
+        0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+        0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+        0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+        0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+        0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+        0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+        0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+        0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+        0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+        0xc67178f2u};
+    u32 a = 0x6a09e667u, b = 0xbb67ae85u, c = 0x3c6ef372u, d = 0xa54ff53au;
+    u32 e = 0x510e527fu, f = 0x9b05688cu, g = 0x1f83d9abu, h = 0x5be0cd19u;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+#endif
+    for (int t = 0; t < 64; ++t) {
+        u32 w;
+        if (t < 16) {
+            w = W[t];
+        } else {
+            u32 w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
+            u32 s0 = hb_rotr(w15, 7) ^ hb_rotr(w15, 18) ^ (w15 >> 3);
+            u32 s1 = hb_rotr(w2, 17) ^ hb_rotr(w2, 19) ^ (w2 >> 10);
+            w = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
+            W[t & 15] = w;
+        }
+        u32 S1 = hb_rotr(e, 6) ^ hb_rotr(e, 11) ^ hb_rotr(e, 25);
+        u32 ch = (e & f) ^ (~e & g);
+        u32 t1 = h + S1 + ch + K[t] + w;
+        u32 S0 = hb_rotr(a, 2) ^ hb_rotr(a, 13) ^ hb_rotr(a, 22);
+        u32 mj = (a & b) ^ (a & c) ^ (b & c);
+        u32 t2 = S0 + mj;
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + t2;
+    }
+    H[0] = a + 0x6a09e667u; H[1] = b + 0xbb67ae85u; H[2] = c + 0x3c6ef372u; H[3] = d + 0xa54ff53au;
+    H[4] = e + 0x510e527fu; H[5] = f + 0x9b05688cu; H[6] = g + 0x1f83d9abu; H[7] = h + 0x5be0cd19u;
+}
+
+// ------------------------------------------------------------------ PRF try
+// Parameters of one KeyedPRF instance (util.py:66-81): AES key schedule and
+// the range R.  R is little-endian in NL u32 limbs; nb = ceil(bitlen(R)/8)
+// keystream bytes per try; topmask masks the most significant output byte.
+template <int NL>
+struct PrfParams {
+    u32 rk[60];
+    u32 R[NL];
+    u32 nb;
+    u32 topmask;
+};
+
+// One rejection-sampling try of KeyedPRF.eval: nb CFB-8 steps continuing the
+// stream held in the shift register sr[0..3] (little-endian words of the 16
+// register bytes).  dig: SHA-256 digest (big-endian words) -- the padded
+// plaintext is dig bytes then zeros (KeyedPRF.pad).  out = mask & BE(ct).
+// Returns 1 if out < R (accepted).
+template <int NL, int NR>
+HB_HD u32 hb_prf_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const u32 dig[8],
+                     u32 out[NL]) {
+    u32 dq[8];
+    for (int t = 0; t < 8; ++t) dq[t] = dig[t];
+    for (int t = 0; t < NL; ++t) out[t] = 0;
+    u32 m = P.topmask;
+    const u32 nw = P.nb >> 2, tail = P.nb & 3u;
+    u32 s0 = sr[0], s1 = sr[1], s2 = sr[2], s3 = sr[3];
+    for (u32 wi = 0; wi <= nw; ++wi) {
+        const u32 nbytes = wi < nw ? 4u : tail;
+        if (nbytes == 0) break;
+        u32 dword = dq[0];
+        for (int t = 0; t < 7; ++t) dq[t] = dq[t + 1];
+        dq[7] = 0;
+        u32 word = 0;
+        for (u32 bi = 0; bi < nbytes; ++bi) {
+            u32 o = hb_aes_byte0<NR>(L, P.rk, s0, s1, s2, s3);
+            u32 c = ((dword >> (24 - 8 * bi)) & 0xffu) ^ o;
+            s0 = hb_alignbit(s1, s0, 8);
+            s1 = hb_alignbit(s2, s1, 8);
+            s2 = hb_alignbit(s3, s2, 8);
+            s3 = (s3 >> 8) | (c << 24);
+            word = (word << 8) | (c & m);
+            m = 0xffu;
+        }
+        if (nbytes == 4) {
+            for (int t = NL - 1; t > 0; --t) out[t] = out[t - 1];
+            out[0] = word;
+        } else {
+            const u32 sh = 32 - 8 * nbytes;   // shift out left by 8*nbytes bits
+            for (int t = NL - 1; t > 0; --t) out[t] = hb_alignbit(out[t], out[t - 1], sh);
+            out[0] = hb_alignbit(out[0], word << sh, sh);
+        }
+    }
+    sr[0] = s0; sr[1] = s1; sr[2] = s2; sr[3] = s3;
+    // out < R  <=>  out - R borrows
+    u32 borrow = 0;
+    for (int t = 0; t < NL; ++t) {
+        u64 d = (u64)out[t] - (u64)P.R[t] - (u64)borrow;
+        borrow = (u32)(d >> 63);
+    }
+    return borrow;
+}
+
+// ------------------------------------------------------------------ mod p
+// p as NL little-endian limbs, Montgomery R = 2^(32 NL), pinv = -p^-1 mod 2^32,
+// inv_scaled = 2^(32 (NL-2)) / p (double) for the final quotient estimate.
+template <int NL>
+struct ModP {
+    u32 p[NL];
+    u32 pinv;
+    u32 pad_;
+    double inv_scaled;
+};
+
+// acc (2NL+1 limbs) += a * b  (a, b: NL limbs).  Product scanning with a
+// 96-bit column accumulator.
+template <int NL>
+HB_HD void hb_mac(u32 acc[2 * NL + 1], const u32 *a, const u32 b[NL]) {
+    u64 lo = 0;
+    u32 hi = 0;
+    for (int t = 0; t < 2 * NL - 1; ++t) {
+        u64 x = lo + acc[t];
+        hi += (u32)(x < lo);
+        lo = x;
+        const int a0 = t < NL ? 0 : t - NL + 1, a1 = t < NL ? t : NL - 1;
+        for (int i = a0; i <= a1; ++i) {
+            u64 pr = (u64)a[i] * b[t - i];
+            u64 y = lo + pr;
+            hi += (u32)(y < lo);
+            lo = y;
+        }
+        acc[t] = (u32)lo;
+        lo = (lo >> 32) | ((u64)hi << 32);
+        hi = 0;
+    }
+    // lo < (NL + 1) 2^32 here: adding one limb cannot wrap 64 bits.
+    u64 x = lo + acc[2 * NL - 1];
+    acc[2 * NL - 1] = (u32)x;
+    acc[2 * NL] += (u32)(x >> 32);
+}
+
+// Montgomery reduction of acc (2NL+1 limbs, value T): v = (T + M p) / R with
+// v < T/R + p, NL+1 limbs.
+template <int NL>
+HB_HD void hb_redc(u32 acc[2 * NL + 1], const ModP<NL> &P, u32 v[NL + 1]) {
+    u32 extra = 0;
+    for (int i = 0; i < NL; ++i) {
+        u32 q = acc[i] * P.pinv;
+        u64 carry = 0;
+        for (int b = 0; b < NL; ++b) {
+            u64 t = (u64)q * P.p[b] + acc[i + b] + carry;
+            acc[i + b] = (u32)t;
+            carry = t >> 32;
+        }
+        u64 t = (u64)acc[i + NL] + carry + extra;
+        acc[i + NL] = (u32)t;
+        extra = (u32)(t >> 32);
+    }
+    acc[2 * NL] += extra;
+    for (int t = 0; t <= NL; ++t) v[t] = acc[NL + t];
+}
+
+template <int E>
+struct HbPow2 {   // 2^(32 E), E >= 0, as a compile-time double
+    static constexpr double v = HbPow2<E - 1>::v * 4294967296.0;
+};
+template <>
+struct HbPow2<0> { static constexpr double v = 1.0; };
+
+// 2^(32 (T - (NL - 2))): limb T of a value scaled so that NL+1 limbs of up to
+// 1056 bits stay inside the double exponent range.
+template <int NL, int T>
+struct HbScale {
+    static constexpr int E = T - (NL - 2);
+    static constexpr double v = E >= 0 ? HbPow2<(E >= 0 ? E : 0)>::v : 1.0 / HbPow2<(E < 0 ? -E : 0)>::v;
+};
+
+// v (NL+1 limbs, v < 2^32 p) -> v mod p in out (NL limbs).
+template <int NL>
+HB_HD void hb_reduce_small(u32 v[NL + 1], const ModP<NL> &P, u32 out[NL]) {
+    double vd = 0.0, sc = HbScale<NL, 0>::v;
+    for (int t = 0; t <= NL; ++t) {
+        vd += (double)v[t] * sc;
+        sc *= 4294967296.0;
+    }
+    double qd = vd * P.inv_scaled;
+    u32 q = qd >= 2.0 ? (u32)qd - 1u : 0u;   // floor(qd) - 1 <= true quotient
+    if (q) {
+        u64 carry = 0;
+        u32 borrow = 0;
+        for (int t = 0; t <= NL; ++t) {
+            u64 pr = (u64)q * (t < NL ? P.p[t] : 0u) + carry;
+            carry = pr >> 32;
+            u64 d = (u64)v[t] - (u32)pr - borrow;
+            v[t] = (u32)d;
+            borrow = (u32)(d >> 63);
+        }
+    }
+    for (;;) {   // at most a few iterations
+        u32 borrow = 0;
+        u32 d[NL + 1];
+        for (int t = 0; t <= NL; ++t) {
+            u64 x = (u64)v[t] - (t < NL ? P.p[t] : 0u) - borrow;
+            d[t] = (u32)x;
+            borrow = (u32)(x >> 63);
+        }
+        if (borrow) break;   // v < p
+        for (int t = 0; t <= NL; ++t) v[t] = d[t];
+    }
+    for (int t = 0; t < NL; ++t) out[t] = v[t];
+}
+
+// ------------------------------------------------------------------ sectors
+// Little-endian limbs of the big-endian integer data[off .. off+r) (r <= 4 NL),
+// byte by byte: used for tail sectors and unaligned sector sizes.
+template <int NL>
+HB_HD void hb_load_be_bytes(const unsigned char *data, u64 off, u32 r, u32 m[NL]) {
+    for (int t = 0; t < NL; ++t) m[t] = 0;
+    for (u32 k = 0; k < r; ++k) {
+        u32 byte = data[off + k];
+        for (int t = NL - 1; t > 0; --t) m[t] = hb_alignbit(m[t], m[t - 1], 24);
+        m[0] = (m[0] << 8) | byte;
+    }
+}
+
+// Whole sector, ss % 4 == 0 and data + off 4-byte aligned.
+template <int NL>
+HB_HD void hb_load_be_words(const unsigned char *data, u64 off, u32 ss, u32 m[NL]) {
+    const u32 nw = ss >> 2;
+    for (int t = 0; t < NL; ++t) {
+        m[t] = 0;
+        if ((u32)t < nw) m[t] = hb_bswap(*(const u32 *)(data + off + ss - 4u * (u32)(t + 1)));
+    }
+}
+
+// Store v (NL limbs) as tw big-endian bytes at dst.
+template <int NL>
+HB_HD void hb_store_be(unsigned char *dst, u32 tw, const u32 v[NL]) {
+    if ((tw & 3u) == 0) {
+        for (int t = 0; t < NL; ++t)
+            if (4u * (u32)(t + 1) <= tw) *(u32 *)(dst + tw - 4u * (u32)(t + 1)) = hb_bswap(v[t]);
+    } else {
+        for (int t = 0; t < NL; ++t)
+            for (int b = 0; b < 4; ++b) {
+                u32 pos = 4u * (u32)t + (u32)b;   // byte index from the least significant end
+                if (pos < tw) dst[tw - 1 - pos] = (unsigned char)(v[t] >> (8 * b));
+            }
+    }
+}
+
+// ------------------------------------------------------------------ block tag
+// Sector loads of a whole block: ALIGN = 16 (ss % 16 == 0, C % 16 == 0, data
+// 16-byte aligned: 16-byte loads), anything else: byte loads.
+template <int NL>
+HB_HD void hb_load_be_16(const unsigned char *data, u64 off, u32 ss, u32 m[NL]) {
+    for (int u = 0; u < NL / 4; ++u) {
+        u32 w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        if (16u * (u32)(u + 1) <= ss) {
+            const u32 *q = (const u32 *)(data + off + ss - 16u * (u32)(u + 1));
+#if defined(__HIP_DEVICE_COMPILE__)
+            uint4 v = *(const uint4 *)q;
+            w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+#else
+            w0 = q[0]; w1 = q[1]; w2 = q[2]; w3 = q[3];
+#endif
+        }
+        m[4 * u + 0] = hb_bswap(w3);
+        m[4 * u + 1] = hb_bswap(w2);
+        m[4 * u + 2] = hb_bswap(w1);
+        m[4 * u + 3] = hb_bswap(w0);
+    }
+}
+
+// tag = (F + sum_j alpha_j m_j) mod p for block `blk` of the call
+// (PySwizzle.py:297-307), with alpha in Montgomery form (alpha_j R mod p):
+//   acc = F R + sum_j (alpha_j R) m_j  <  (S+1) p R
+//   REDC(acc) = F + sum_j alpha_j m_j (mod p),  < (S+2) p
+// then one small quotient-estimate reduction.  Sector j of the block is
+// data[blk*C + j*ss : min(.. + ss, len)] as a big-endian integer (0 if empty);
+// sectors after a short one are empty by construction, which is the
+// reference's break at the first short read (PySwizzle.py:304-306).
+template <int NL, int ALIGN>
+HB_HD void hb_block_tag(const unsigned char *data, u64 len, u64 blk, u64 C, u32 ss, u32 S,
+                        const u32 *alpha_mont, const ModP<NL> &M, const u32 F[NL], u32 tag[NL]) {
+    u32 acc[2 * NL + 1];
+    for (int t = 0; t < NL; ++t) { acc[t] = 0; acc[NL + t] = F[t]; }
+    acc[2 * NL] = 0;
+    const u64 base = blk * C;
+    u32 m[NL];
+    if (base + C <= len) {
+        for (u32 j = 0; j < S; ++j) {
+            if (ALIGN == 16) hb_load_be_16<NL>(data, base + (u64)j * ss, ss, m);
+            else hb_load_be_bytes<NL>(data, base + (u64)j * ss, ss, m);
+            hb_mac<NL>(acc, alpha_mont + (u64)j * NL, m);
+        }
+    } else {
+        for (u32 j = 0; j < S; ++j) {
+            const u64 off = base + (u64)j * ss;
+            if (off >= len) break;
+            const u32 r = (u32)(len - off < ss ? len - off : ss);
+            hb_load_be_bytes<NL>(data, off, r, m);
+            hb_mac<NL>(acc, alpha_mont + (u64)j * NL, m);
+            if (r != ss) break;
+        }
+    }
+    u32 v[NL + 1];
+    hb_redc<NL>(acc, M, v);
+    hb_reduce_small<NL>(v, M, tag);
+}
+
+// x R mod p (x < R): REDC(x * (R^2 mod p)).
+template <int NL>
+HB_HD void hb_to_mont(const u32 x[NL], const u32 *r2, const ModP<NL> &M, u32 out[NL]) {
+    u32 acc[2 * NL + 1];
+    for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
+    hb_mac<NL>(acc, r2, x);
+    u32 v[NL + 1];
+    hb_redc<NL>(acc, M, v);
+    hb_reduce_small<NL>(v, M, out);
+}

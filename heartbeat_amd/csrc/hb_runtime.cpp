@@ -1,0 +1,721 @@
+// hb_runtime.cpp -- host runtime and C ABI of libhbswizzle.so (include/hbswizzle.h).
+//
+// Owns per-device state (stream, the global T0 table, job-queue counters,
+// scratch buffers), prepares the uniform kernel arguments (AES key schedule,
+// range, Montgomery constants), stages host data through the GPU in chunks
+// (H2D copies on a copy stream overlapped with encode kernels on the compute
+// stream), and converts results to big-endian byte strings.  All per-block and
+// per-challenge arithmetic runs in the kernels of hb_kernels.hip; there is no
+// CPU compute path.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <vector>
+
+#include "../../include/hbswizzle.h"
+#include "hb_aes_host.hpp"
+#include "hb_args.hpp"
+#include "hb_bignum_host.hpp"
+
+using namespace hbhost;
+
+// launchers (hb_kernels.hip)
+template <int NL> hipError_t hb_launch_encode(const EncodeArgs<NL> &, int, int, int, hipStream_t);
+template <int NL> hipError_t hb_launch_prf(const PrfArgs<NL> &, int, int, hipStream_t);
+template <int NL> hipError_t hb_launch_mont(const MontArgs<NL> &, hipStream_t);
+template <int NL> hipError_t hb_launch_wsum(const WsumArgs<NL> &, int, int, hipStream_t);
+template <int NL> hipError_t hb_launch_sum(const SumArgs<NL> &, int, hipStream_t);
+hipError_t hb_launch_fill(unsigned char *, u64, u64, hipStream_t);
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(&p, want ? want : 1);
+        if (e == hipSuccess) n = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+struct hb_ctx {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr, copy = nullptr;
+    hipEvent_t k0 = nullptr, k1 = nullptr;
+    hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    u32 *t0 = nullptr;
+    unsigned long long *queue = nullptr;   // 16 slots of HB_QSLOT counters
+    DevBuf alpha_raw, alpha_mont, xs, vals, vals2, wts, idx, partials, sums, data[2], tags, blen, gtags;
+    std::string err;
+    double last_ms = 0.0;
+    u32 last_launches = 0;
+};
+
+namespace {
+
+int fail(hb_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+int hipfail(hb_ctx *c, hipError_t e, const char *what) {
+    return fail(c, HB_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HB_CHECK(expr, what)                         \
+    do {                                             \
+        hipError_t e_ = (expr);                      \
+        if (e_ != hipSuccess) return hipfail(c, e_, what); \
+    } while (0)
+
+int nl_for_bits(int bits) {
+    if (bits <= 64) return 2;
+    if (bits <= 256) return 8;
+    if (bits <= 512) return 16;
+    if (bits <= 1024) return 32;
+    return 0;
+}
+
+template <int NL>
+bool make_prf(const uint8_t *key, size_t key_len, const uint8_t *range_be, size_t range_len,
+              PrfParams<NL> &P, int &nr) {
+    AesKey k;
+    if (!aes_expand(key, key_len, k)) return false;
+    nr = k.nr;
+    memset(&P, 0, sizeof P);
+    memcpy(P.rk, k.rk, sizeof(u32) * 4 * (size_t)(k.nr + 1));
+    Limbs R = from_be(range_be, range_len, NL);
+    for (int t = 0; t < NL; ++t) P.R[t] = R[t];
+    int bits = bitlen_be(range_be, range_len);
+    P.nb = (u32)(bits + 7) / 8;
+    P.topmask = (1u << (bits - 8 * ((int)P.nb - 1))) - 1u;
+    return true;
+}
+
+template <int NL>
+void make_mod(const Limbs &p, ModP<NL> &M) {
+    memset(&M, 0, sizeof M);
+    for (int t = 0; t < NL; ++t) M.p[t] = p[t];
+    M.pinv = mont_pinv(p[0]);
+    M.inv_scaled = inv_scaled(p);
+}
+
+int engine_grid(hb_ctx *c, u64 njobs) {
+    u64 g = (njobs + HB_ENGINE_WG - 1) / HB_ENGINE_WG;
+    u64 cap = 2ull * (u64)c->num_cus;
+    if (g > cap) g = cap;
+    return (int)(g ? g : 1);
+}
+
+int check_key(hb_ctx *c, size_t key_len) {
+    if (key_len != 16 && key_len != 24 && key_len != 32)
+        return fail(c, HB_EINVAL, "AES key must be either 16, 24, or 32 bytes long");
+    return 0;
+}
+
+// KeyedPRF(key, range).eval(x) for n inputs (xs device array or x0 + k),
+// results as NL-limb little-endian values in out (device).
+template <int NL>
+int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be, size_t range_len,
+            const u64 *xs_dev, u64 x0, u64 n, u32 *out_dev, int queue_slot) {
+    PrfArgs<NL> A;
+    int nr = 0;
+    if (!make_prf<NL>(key, key_len, range_be, range_len, A.prf, nr))
+        return fail(c, HB_EINVAL, "invalid PRF key");
+    A.xs = xs_dev;
+    A.x0 = x0;
+    A.n = n;
+    A.out = out_dev;
+    A.t0 = c->t0;
+    A.queue = c->queue + HB_QSLOT * queue_slot;
+    if (n == 0) return 0;
+    HB_CHECK(hipMemsetAsync(A.queue, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+    HB_CHECK(hb_launch_prf<NL>(A, nr, engine_grid(c, n), c->stream), "hb_prf_kernel launch");
+    return 0;
+}
+
+// After a synchronize: did any PRF launch abandon a job (queue slot [2])?
+int check_prf_slots(hb_ctx *c) {
+    unsigned long long q[16 * HB_QSLOT];
+    HB_CHECK(hipMemcpy(q, c->queue, sizeof q, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
+    for (int s = 0; s < 16; ++s)
+        if (q[s * HB_QSLOT + 2]) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate");
+    return 0;
+}
+
+// in (n x NL limbs, device) -> in * R mod p (device)
+template <int NL>
+int run_mont(hb_ctx *c, const Limbs &p, const u32 *in, u32 *out, u64 n) {
+    if (n == 0) return 0;
+    MontArgs<NL> A;
+    make_mod<NL>(p, A.mod);
+    Limbs r2 = pow2_mod(64u * NL, p);
+    for (int t = 0; t < NL; ++t) A.r2[t] = r2[t];
+    A.in = in;
+    A.out = out;
+    A.n = n;
+    HB_CHECK(hb_launch_mont<NL>(A, c->stream), "hb_mont_kernel launch");
+    return 0;
+}
+
+struct PrimeInfo {
+    int bits = 0, nl = 0;
+    u32 ss = 0, tw = 0;
+};
+
+int parse_prime(hb_ctx *c, const uint8_t *p_be, size_t p_len, PrimeInfo &pi) {
+    if (!p_be || p_len == 0) return fail(c, HB_EINVAL, "prime is empty");
+    pi.bits = bitlen_be(p_be, p_len);
+    if (pi.bits < 9) return fail(c, HB_EINVAL, "prime must be at least 2^8 (sector size >= 1 byte)");
+    if (!(p_be[p_len - 1] & 1)) return fail(c, HB_EINVAL, "prime must be odd");
+    pi.nl = nl_for_bits(pi.bits);
+    if (pi.nl < 8) pi.nl = 8;
+    if (!pi.nl || pi.bits > 1024)
+        return fail(c, HB_EUNSUPPORTED, "primes above 1024 bits are not supported by this build");
+    pi.ss = (u32)pi.bits / 8;
+    pi.tw = (u32)(pi.bits + 7) / 8;
+    return 0;
+}
+
+// ------------------------------------------------------------------ encode
+template <int NL>
+int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
+                const uint8_t *f_key, const uint8_t *a_key, size_t key_len, u64 block_base,
+                const uint8_t *data, u64 len, u64 nblocks, uint8_t *tags, u32 flags, u64 *tries_out) {
+    Limbs p = from_be(p_be, p_len, NL);
+    const u64 C = (u64)pi.ss * S;
+    // alpha_j R mod p, j < S  (alpha = KeyedPRF(alpha_key, p), PySwizzle.py:291,302)
+    HB_CHECK(c->alpha_raw.ensure((size_t)S * NL * 4), "hipMalloc");
+    HB_CHECK(c->alpha_mont.ensure((size_t)S * NL * 4), "hipMalloc");
+    int rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1);
+    if (rc) return rc;
+    rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S);
+    if (rc) return rc;
+
+    EncodeArgs<NL> A;
+    int nr = 0;
+    if (!make_prf<NL>(f_key, key_len, p_be, p_len, A.prf, nr)) return fail(c, HB_EINVAL, "invalid key");
+    make_mod<NL>(p, A.mod);
+    A.alpha_mont = (const u32 *)c->alpha_mont.p;
+    A.t0 = c->t0;
+    A.queue = c->queue;
+    A.C = C;
+    A.tw = pi.tw;
+    A.ss = pi.ss;
+    A.S = S;
+    A.pad_ = 0;
+    HB_CHECK(hipMemsetAsync(c->queue, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+
+    const bool tags_dev = flags & HB_TAGS_ON_DEVICE;
+    uint8_t *dtags = tags;
+    if (!tags_dev) {
+        HB_CHECK(c->tags.ensure((size_t)(nblocks * pi.tw)), "hipMalloc(tags)");
+        dtags = (uint8_t *)c->tags.p;
+    }
+    c->last_launches = 0;
+    float ms_total = 0.f;
+
+    auto launch = [&](const uint8_t *d, u64 dlen, u64 nb, u64 base, uint8_t *tg) -> int {
+        A.data = d;
+        A.len = dlen;
+        A.nblocks = nb;
+        A.block_base = base;
+        A.tags = tg;
+        const int align = (pi.ss % 16 == 0 && C % 16 == 0 && ((uintptr_t)d % 16) == 0) ? 16 : 1;
+        // queue[0] is the per-launch job counter; queue[1] accumulates tries
+        HB_CHECK(hipMemsetAsync(c->queue, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+        HB_CHECK(hb_launch_encode<NL>(A, nr, align, engine_grid(c, nb), c->stream), "hb_encode_kernel launch");
+        c->last_launches++;
+        return 0;
+    };
+
+    if (flags & HB_DATA_ON_DEVICE) {
+        HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
+        rc = launch(data, len, nblocks, block_base, dtags);
+        if (rc) return rc;
+        HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
+        HB_CHECK(hipEventSynchronize(c->k1), "encode");
+        HB_CHECK(hipEventElapsedTime(&ms_total, c->k0, c->k1), "hipEventElapsedTime");
+    } else {
+        // Host bytes: chunks of whole blocks double-buffered through the GPU,
+        // H2D on the copy stream overlapping the encode kernel of the previous
+        // chunk on the compute stream.
+        const u64 target = 256ull << 20;
+        u64 cb = C ? target / C : 1;
+        if (cb < 1) cb = 1;
+        HB_CHECK(c->data[0].ensure((size_t)(cb * C)), "hipMalloc(staging)");
+        HB_CHECK(c->data[1].ensure((size_t)(cb * C)), "hipMalloc(staging)");
+        HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
+        for (u64 k0 = 0, it = 0; k0 < nblocks; k0 += cb, ++it) {
+            const int b = (int)(it & 1);
+            const u64 nb = nblocks - k0 < cb ? nblocks - k0 : cb;
+            const u64 off = k0 * C;
+            const u64 end = (k0 + nb) * C < len ? (k0 + nb) * C : len;
+            const u64 bytes = end > off ? end - off : 0;
+            if (it >= 2) HB_CHECK(hipStreamWaitEvent(c->copy, c->done[b], 0), "hipStreamWaitEvent");
+            if (bytes)
+                HB_CHECK(hipMemcpyAsync(c->data[b].p, data + off, (size_t)bytes, hipMemcpyHostToDevice, c->copy),
+                         "hipMemcpyAsync(H2D)");
+            HB_CHECK(hipEventRecord(c->copied[b], c->copy), "hipEventRecord");
+            HB_CHECK(hipStreamWaitEvent(c->stream, c->copied[b], 0), "hipStreamWaitEvent");
+            rc = launch((const uint8_t *)c->data[b].p, bytes, nb, block_base + k0, dtags + k0 * pi.tw);
+            if (rc) return rc;
+            HB_CHECK(hipEventRecord(c->done[b], c->stream), "hipEventRecord");
+        }
+        HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
+        HB_CHECK(hipEventSynchronize(c->k1), "encode");
+        HB_CHECK(hipEventElapsedTime(&ms_total, c->k0, c->k1), "hipEventElapsedTime");
+    }
+    c->last_ms = ms_total;
+    if (!tags_dev)
+        HB_CHECK(hipMemcpy(tags, dtags, (size_t)(nblocks * pi.tw), hipMemcpyDeviceToHost), "hipMemcpy(tags)");
+    unsigned long long q[HB_QSLOT];
+    HB_CHECK(hipMemcpy(q, c->queue, sizeof q, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
+    if (q[2]) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate for some blocks");
+    if (tries_out) *tries_out = q[1];
+    return check_prf_slots(c);
+}
+
+// ------------------------------------------------------------------ sums
+// Finish a wsum launch: reduce the partials of each column and return the
+// results as big-endian tw-byte values in out (host).
+template <int NL>
+int finish_sums(hb_ctx *c, const Limbs &p, u32 ncols, u32 nparts, u32 tw, uint8_t *out) {
+    SumArgs<NL> A;
+    make_mod<NL>(p, A.mod);
+    A.partials = (const u32 *)c->partials.p;
+    A.nparts = nparts;
+    HB_CHECK(c->sums.ensure((size_t)ncols * NL * 4), "hipMalloc");
+    A.out = (u32 *)c->sums.p;
+    HB_CHECK(hb_launch_sum<NL>(A, (int)ncols, c->stream), "hb_sum_kernel launch");
+    std::vector<u32> h((size_t)ncols * NL);
+    HB_CHECK(hipMemcpyAsync(h.data(), c->sums.p, h.size() * 4, hipMemcpyDeviceToHost, c->stream), "hipMemcpy");
+    HB_CHECK(hipStreamSynchronize(c->stream), "sum");
+    for (u32 k = 0; k < ncols; ++k) to_be(&h[(size_t)k * NL], NL, out + (size_t)k * tw, tw);
+    return check_prf_slots(c);
+}
+
+u32 wsum_grid(u64 nterms) {
+    u64 g = (nterms + 255) / 256;
+    if (g > 1024) g = 1024;
+    return (u32)(g ? g : 1);
+}
+
+int u64_be(u64 v, uint8_t out[8]) {
+    for (int k = 0; k < 8; ++k) out[k] = (uint8_t)(v >> (56 - 8 * k));
+    return 0;
+}
+
+// ------------------------------------------------------------------ prove
+template <int NL>
+int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
+               const uint8_t *chal_key, size_t key_len, u64 chunks, const uint8_t *vmax_be,
+               size_t vmax_len, const uint8_t *tags, u64 ntags, const uint8_t *data, u64 len,
+               u32 flags, uint8_t *mu_out, uint8_t *sigma_out) {
+    Limbs p = from_be(p_be, p_len, NL);
+    const u64 C = (u64)pi.ss * S;
+    const u32 ncols = S + 1;
+    if (chunks == 0) {
+        memset(mu_out, 0, (size_t)S * pi.tw);
+        memset(sigma_out, 0, pi.tw);
+        return 0;
+    }
+    // idx_i = KeyedPRF(key, ntags)(i), v_i = KeyedPRF(key, v_max)(i)   (PySwizzle.py:344-345)
+    uint8_t nbe[8];
+    u64_be(ntags, nbe);
+    HB_CHECK(c->idx.ensure((size_t)chunks * 8), "hipMalloc(idx)");
+    HB_CHECK(c->vals.ensure((size_t)chunks * NL * 4), "hipMalloc(v)");
+    HB_CHECK(c->wts.ensure((size_t)chunks * NL * 4), "hipMalloc(w)");
+    int rc = run_prf<2>(c, chal_key, key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 2);
+    if (rc) return rc;
+    rc = run_prf<NL>(c, chal_key, key_len, vmax_be, vmax_len, nullptr, 0, chunks, (u32 *)c->vals.p, 3);
+    if (rc) return rc;
+    rc = run_mont<NL>(c, p, (const u32 *)c->vals.p, (u32 *)c->wts.p, chunks);
+    if (rc) return rc;
+
+    WsumArgs<NL> A;
+    memset(&A, 0, sizeof A);
+    make_mod<NL>(p, A.mod);
+    A.ncols = ncols;
+    A.idx = (const u64 *)c->idx.p;
+    A.w = (const u32 *)c->wts.p;
+    A.nterms = chunks;
+    A.C = C;
+    A.ss = pi.ss;
+    A.S = S;
+    A.tw = pi.tw;
+    const u32 gx = wsum_grid(chunks);
+    const u32 nparts = gx * 256;
+    HB_CHECK(c->partials.ensure((size_t)ncols * nparts * NL * 4), "hipMalloc(partials)");
+    A.partials = (u32 *)c->partials.p;
+
+    const bool data_dev = flags & HB_DATA_ON_DEVICE, tags_dev = flags & HB_TAGS_ON_DEVICE;
+    int align = 1;
+    if (data_dev && tags_dev) {
+        A.mode = 0;
+        A.data = data;
+        A.len = len;
+        A.tags = tags;
+        align = (pi.ss % 16 == 0 && C % 16 == 0 && ((uintptr_t)data % 16) == 0) ? 16 : 1;
+    } else {
+        // Gather the challenged blocks (and their tags) on the host -- the
+        // reference's file.seek/read per index (PySwizzle.py:353-355) -- and
+        // ship only those to the GPU.
+        std::vector<u64> hidx(chunks);
+        HB_CHECK(hipMemcpyAsync(hidx.data(), c->idx.p, (size_t)chunks * 8, hipMemcpyDeviceToHost, c->stream),
+                 "hipMemcpy(idx)");
+        HB_CHECK(hipStreamSynchronize(c->stream), "prf");
+        std::vector<uint8_t> gblocks((size_t)(chunks * C)), gtags((size_t)chunks * pi.tw);
+        std::vector<u64> blen(chunks);
+        std::vector<uint8_t> tagbuf;
+        if (tags_dev) {   // rare: device tags with host data
+            tagbuf.resize((size_t)(ntags * pi.tw));
+            HB_CHECK(hipMemcpy(tagbuf.data(), tags, tagbuf.size(), hipMemcpyDeviceToHost), "hipMemcpy(tags)");
+        }
+        const uint8_t *htags = tags_dev ? tagbuf.data() : tags;
+        std::vector<uint8_t> blkbuf;
+        for (u64 i = 0; i < chunks; ++i) {
+            const u64 ix = hidx[i];
+            if (ix >= ntags) return fail(c, HB_EINVAL, "internal: index out of range");
+            const u64 off = ix * C;
+            const u64 n = off >= len ? 0 : (len - off < C ? len - off : C);
+            blen[i] = n;
+            if (n) {
+                if (data_dev) {
+                    HB_CHECK(hipMemcpy(&gblocks[(size_t)(i * C)], data + off, (size_t)n, hipMemcpyDeviceToHost),
+                             "hipMemcpy(block)");
+                } else {
+                    memcpy(&gblocks[(size_t)(i * C)], data + off, (size_t)n);
+                }
+            }
+            memcpy(&gtags[(size_t)i * pi.tw], htags + ix * pi.tw, pi.tw);
+        }
+        HB_CHECK(c->data[0].ensure(gblocks.size()), "hipMalloc");
+        HB_CHECK(c->gtags.ensure(gtags.size()), "hipMalloc");
+        HB_CHECK(c->blen.ensure(blen.size() * 8), "hipMalloc");
+        HB_CHECK(hipMemcpyAsync(c->data[0].p, gblocks.data(), gblocks.size(), hipMemcpyHostToDevice, c->stream), "H2D");
+        HB_CHECK(hipMemcpyAsync(c->gtags.p, gtags.data(), gtags.size(), hipMemcpyHostToDevice, c->stream), "H2D");
+        HB_CHECK(hipMemcpyAsync(c->blen.p, blen.data(), blen.size() * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+        A.mode = 2;
+        A.data = (const unsigned char *)c->data[0].p;
+        A.len = chunks * C;
+        A.tags = (const unsigned char *)c->gtags.p;
+        A.blen = (const u64 *)c->blen.p;
+        // gathered tags are addressed by position i: identity index
+        std::vector<u64> iota(chunks);
+        for (u64 i = 0; i < chunks; ++i) iota[i] = i;
+        HB_CHECK(c->xs.ensure((size_t)chunks * 8), "hipMalloc");
+        HB_CHECK(hipMemcpyAsync(c->xs.p, iota.data(), (size_t)chunks * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+        A.idx = (const u64 *)c->xs.p;
+        align = (pi.ss % 16 == 0 && C % 16 == 0) ? 16 : 1;
+        HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");
+        std::vector<uint8_t> out((size_t)ncols * pi.tw);
+        rc = finish_sums<NL>(c, p, ncols, nparts, pi.tw, out.data());
+        if (rc) return rc;
+        memcpy(mu_out, out.data(), (size_t)S * pi.tw);
+        memcpy(sigma_out, out.data() + (size_t)S * pi.tw, pi.tw);
+        return 0;
+    }
+    HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");
+    std::vector<uint8_t> out((size_t)ncols * pi.tw);
+    rc = finish_sums<NL>(c, p, ncols, nparts, pi.tw, out.data());
+    if (rc) return rc;
+    memcpy(mu_out, out.data(), (size_t)S * pi.tw);
+    memcpy(sigma_out, out.data() + (size_t)S * pi.tw, pi.tw);
+    return 0;
+}
+
+// ------------------------------------------------------------------ verify
+template <int NL>
+int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
+                const uint8_t *f_key, const uint8_t *a_key, size_t key_len, u64 state_chunks,
+                const uint8_t *chal_key, size_t chal_key_len, u64 chunks, const uint8_t *vmax_be,
+                size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out) {
+    Limbs p = from_be(p_be, p_len, NL);
+    const u64 nterms = chunks + S;
+    uint8_t nbe[8];
+    u64_be(state_chunks, nbe);
+    HB_CHECK(c->idx.ensure((size_t)(chunks ? chunks : 1) * 8), "hipMalloc");
+    HB_CHECK(c->vals.ensure((size_t)nterms * NL * 4), "hipMalloc");   // raw v_i | alpha_j
+    HB_CHECK(c->wts.ensure((size_t)nterms * NL * 4), "hipMalloc");    // Montgomery weights
+    HB_CHECK(c->vals2.ensure((size_t)nterms * NL * 4), "hipMalloc");  // F(idx_i) | mu_j
+    u32 *raw = (u32 *)c->vals.p, *w = (u32 *)c->wts.p, *val = (u32 *)c->vals2.p;
+    int rc = 0;
+    if (chunks) {
+        // index = KeyedPRF(key, state.chunks), v = KeyedPRF(key, v_max)   (PySwizzle.py:381-382)
+        rc = run_prf<2>(c, chal_key, chal_key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 2);
+        if (rc) return rc;
+        rc = run_prf<NL>(c, chal_key, chal_key_len, vmax_be, vmax_len, nullptr, 0, chunks, raw, 3);
+        if (rc) return rc;
+        // f.eval(index.eval(i))   (PySwizzle.py:389)
+        rc = run_prf<NL>(c, f_key, key_len, p_be, p_len, (const u64 *)c->idx.p, 0, chunks, val, 4);
+        if (rc) return rc;
+    }
+    // alpha.eval(j)   (PySwizzle.py:392)
+    rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, raw + chunks * NL, 5);
+    if (rc) return rc;
+    rc = run_mont<NL>(c, p, raw, w, nterms);
+    if (rc) return rc;
+    std::vector<u32> hmu((size_t)S * NL);
+    for (u32 j = 0; j < S; ++j) {
+        Limbs m = from_be(mu + (size_t)j * pi.tw, pi.tw, NL);
+        memcpy(&hmu[(size_t)j * NL], m.data(), NL * 4);
+    }
+    HB_CHECK(hipMemcpyAsync(val + chunks * NL, hmu.data(), hmu.size() * 4, hipMemcpyHostToDevice, c->stream), "H2D");
+    WsumArgs<NL> A;
+    memset(&A, 0, sizeof A);
+    make_mod<NL>(p, A.mod);
+    A.mode = 1;
+    A.ncols = 1;
+    A.w = w;
+    A.vals = val;
+    A.nterms = nterms;
+    A.S = S;
+    const u32 gx = wsum_grid(nterms);
+    const u32 nparts = gx * 256;
+    HB_CHECK(c->partials.ensure((size_t)nparts * NL * 4), "hipMalloc(partials)");
+    A.partials = (u32 *)c->partials.p;
+    HB_CHECK(hb_launch_wsum<NL>(A, 1, (int)gx, c->stream), "hb_wsum_kernel launch");
+    return finish_sums<NL>(c, p, 1, nparts, pi.tw, rhs_out);
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+int hb_abi_version(void) { return HB_ABI_VERSION; }
+
+int hb_ctx_create(int device, hb_ctx **out) {
+    if (!out) return HB_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) {
+        g_create_error = std::string("no usable HIP device: ") + (e != hipSuccess ? hipGetErrorString(e) : "0 devices");
+        return HB_EHIP;
+    }
+    if (device < 0 || device >= ndev) {
+        g_create_error = "device ordinal out of range";
+        return HB_EINVAL;
+    }
+    hb_ctx *c = new hb_ctx();
+    c->device = device;
+    auto bad = [&](hipError_t err, const char *what) {
+        g_create_error = std::string(what) + ": " + hipGetErrorString(err);
+        hb_ctx_destroy(c);
+        return HB_EHIP;
+    };
+    if ((e = hipSetDevice(device)) != hipSuccess) return bad(e, "hipSetDevice");
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return bad(e, "hipGetDeviceProperties");
+    if (!strstr(prop.gcnArchName, "gfx950")) {
+        g_create_error = std::string("libhbswizzle is built for gfx950 (MI355X); device is ") + prop.gcnArchName;
+        hb_ctx_destroy(c);
+        return HB_EUNSUPPORTED;
+    }
+    c->num_cus = prop.multiProcessorCount;
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    if ((e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    if ((e = hipEventCreate(&c->k0)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreate(&c->k1)) != hipSuccess) return bad(e, "hipEventCreate");
+    for (int b = 0; b < 2; ++b) {
+        if ((e = hipEventCreateWithFlags(&c->copied[b], hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+        if ((e = hipEventCreateWithFlags(&c->done[b], hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    }
+    if ((e = hipMalloc(&c->t0, 256 * sizeof(u32))) != hipSuccess) return bad(e, "hipMalloc");
+    if ((e = hipMemcpy(c->t0, aes_tables().t0, 256 * sizeof(u32), hipMemcpyHostToDevice)) != hipSuccess)
+        return bad(e, "hipMemcpy");
+    if ((e = hipMalloc(&c->queue, 16 * HB_QSLOT * sizeof(unsigned long long))) != hipSuccess) return bad(e, "hipMalloc");
+    if ((e = hipMemset(c->queue, 0, 16 * HB_QSLOT * sizeof(unsigned long long))) != hipSuccess) return bad(e, "hipMemset");
+    *out = c;
+    return HB_OK;
+}
+
+void hb_ctx_destroy(hb_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->copy) (void)hipStreamSynchronize(c->copy);
+    DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
+                      &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags};
+    for (DevBuf *b : bufs) b->release();
+    if (c->t0) (void)hipFree(c->t0);
+    if (c->queue) (void)hipFree(c->queue);
+    if (c->k0) (void)hipEventDestroy(c->k0);
+    if (c->k1) (void)hipEventDestroy(c->k1);
+    for (int b = 0; b < 2; ++b) {
+        if (c->copied[b]) (void)hipEventDestroy(c->copied[b]);
+        if (c->done[b]) (void)hipEventDestroy(c->done[b]);
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->copy) (void)hipStreamDestroy(c->copy);
+    delete c;
+}
+
+const char *hb_last_error(const hb_ctx *c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+
+size_t hb_width(const uint8_t *p_be, size_t p_len) { return (size_t)(bitlen_be(p_be, p_len) + 7) / 8; }
+
+uint64_t hb_block_count(const uint8_t *p_be, size_t p_len, uint32_t sectors, uint64_t len) {
+    u64 ss = (u64)bitlen_be(p_be, p_len) / 8;
+    u64 C = ss * sectors;
+    return C ? len / C + 1 : 0;
+}
+
+int hb_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be,
+                size_t range_len, const uint64_t *xs, size_t n, uint8_t *out) {
+    if (!c) return HB_EINVAL;
+    if (int rc = check_key(c, key_len)) return rc;
+    const int bits = bitlen_be(range_be, range_len);
+    if (bits == 0) return fail(c, HB_EINVAL, "PRF range must be positive");
+    const int nl = nl_for_bits(bits);
+    if (!nl) return fail(c, HB_EUNSUPPORTED, "PRF ranges above 1024 bits are not supported by this build");
+    if (n == 0) return 0;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    HB_CHECK(c->xs.ensure(n * 8), "hipMalloc");
+    HB_CHECK(c->vals.ensure(n * (size_t)nl * 4), "hipMalloc");
+    HB_CHECK(hipMemcpyAsync(c->xs.p, xs, n * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+    int rc = 0;
+    switch (nl) {
+    case 2: rc = run_prf<2>(c, key, key_len, range_be, range_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6); break;
+    case 8: rc = run_prf<8>(c, key, key_len, range_be, range_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6); break;
+    case 16: rc = run_prf<16>(c, key, key_len, range_be, range_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6); break;
+    default: rc = run_prf<32>(c, key, key_len, range_be, range_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6); break;
+    }
+    if (rc) return rc;
+    std::vector<u32> h(n * (size_t)nl);
+    HB_CHECK(hipMemcpyAsync(h.data(), c->vals.p, h.size() * 4, hipMemcpyDeviceToHost, c->stream), "D2H");
+    HB_CHECK(hipStreamSynchronize(c->stream), "hb_prf_kernel");
+    if (int rc2 = check_prf_slots(c)) return rc2;
+    const size_t nb = (size_t)(bits + 7) / 8;
+    for (size_t i = 0; i < n; ++i) to_be(&h[i * nl], (size_t)nl, out + i * nb, nb);
+    return 0;
+}
+
+int hb_encode(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+              const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
+              uint64_t block_base, const uint8_t *data, uint64_t len,
+              uint64_t nblocks, uint8_t *tags, uint32_t flags, uint64_t *tries_out) {
+    if (!c) return HB_EINVAL;
+    PrimeInfo pi;
+    if (int rc = parse_prime(c, p_be, p_len, pi)) return rc;
+    if (int rc = check_key(c, key_len)) return rc;
+    if (sectors == 0) return fail(c, HB_EINVAL, "sectors must be positive");
+    if (!tags && nblocks) return fail(c, HB_EINVAL, "tags buffer is NULL");
+    if (!data && len) return fail(c, HB_EINVAL, "data buffer is NULL");
+    if (tries_out) *tries_out = 0;
+    if (nblocks == 0) return 0;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    switch (pi.nl) {
+    case 8: return encode_impl<8>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
+    case 16: return encode_impl<16>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
+    default: return encode_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
+    }
+}
+
+int hb_prove(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+             const uint8_t *chal_key, size_t key_len, uint64_t chunks,
+             const uint8_t *vmax_be, size_t vmax_len, const uint8_t *tags, uint64_t ntags,
+             const uint8_t *data, uint64_t len, uint32_t flags, uint8_t *mu_out, uint8_t *sigma_out) {
+    if (!c) return HB_EINVAL;
+    PrimeInfo pi;
+    if (int rc = parse_prime(c, p_be, p_len, pi)) return rc;
+    if (int rc = check_key(c, key_len)) return rc;
+    if (sectors == 0) return fail(c, HB_EINVAL, "sectors must be positive");
+    if (ntags == 0) return fail(c, HB_EINVAL, "tag is empty");
+    const int vbits = bitlen_be(vmax_be, vmax_len);
+    if (vbits == 0) return fail(c, HB_EINVAL, "v_max must be positive");
+    if (vbits > 32 * pi.nl) return fail(c, HB_EUNSUPPORTED, "v_max wider than the prime's limb count");
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    switch (pi.nl) {
+    case 8: return prove_impl<8>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    case 16: return prove_impl<16>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    default: return prove_impl<32>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    }
+}
+
+int hb_verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                  const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
+                  uint64_t state_chunks, const uint8_t *chal_key, size_t chal_key_len, uint64_t chunks,
+                  const uint8_t *vmax_be, size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out) {
+    if (!c) return HB_EINVAL;
+    PrimeInfo pi;
+    if (int rc = parse_prime(c, p_be, p_len, pi)) return rc;
+    if (int rc = check_key(c, key_len)) return rc;
+    if (int rc = check_key(c, chal_key_len)) return rc;
+    if (sectors == 0) return fail(c, HB_EINVAL, "sectors must be positive");
+    if (chunks && state_chunks == 0) return fail(c, HB_EINVAL, "state has no chunks");
+    const int vbits = bitlen_be(vmax_be, vmax_len);
+    if (chunks && vbits == 0) return fail(c, HB_EINVAL, "v_max must be positive");
+    if (vbits > 32 * pi.nl) return fail(c, HB_EUNSUPPORTED, "v_max wider than the prime's limb count");
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    switch (pi.nl) {
+    case 8: return verify_impl<8>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out);
+    case 16: return verify_impl<16>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out);
+    default: return verify_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out);
+    }
+}
+
+int hb_aes_cfb8(const uint8_t *key, size_t key_len, const uint8_t *iv, const uint8_t *in,
+                uint8_t *out, size_t n, int encrypt) {
+    AesKey k;
+    if (!aes_expand(key, key_len, k)) return HB_EINVAL;
+    aes_cfb8(k, iv, in, out, n, encrypt != 0);
+    return 0;
+}
+
+int hb_last_kernel_ms(const hb_ctx *c, double *ms, uint32_t *launches) {
+    if (!c) return HB_EINVAL;
+    if (ms) *ms = c->last_ms;
+    if (launches) *launches = c->last_launches;
+    return 0;
+}
+
+int hb_fill_random(hb_ctx *c, uint8_t *dev_ptr, uint64_t len, uint64_t seed) {
+    if (!c) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    HB_CHECK(hb_launch_fill(dev_ptr, len, seed, c->stream), "hb_fill_kernel launch");
+    HB_CHECK(hipStreamSynchronize(c->stream), "hb_fill_kernel");
+    return 0;
+}
+
+int hb_device_malloc(hb_ctx *c, uint64_t bytes, void **out) {
+    if (!c || !out) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    HB_CHECK(hipMalloc(out, bytes ? bytes : 1), "hipMalloc");
+    return 0;
+}
+
+int hb_device_free(hb_ctx *c, void *p) {
+    if (!c) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    HB_CHECK(hipFree(p), "hipFree");
+    return 0;
+}
+
+int hb_memcpy(hb_ctx *c, void *dst, const void *src, uint64_t bytes, int kind) {
+    if (!c) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HB_CHECK(hipMemcpy(dst, src, bytes, k), "hipMemcpy");
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+"""Shared helpers mirroring heartbeat/util.py: base64 helpers (:30-41) and
+KeyedPRF (:44-96), whose eval runs on the GPU (hb_prf_eval)."""
+import base64
+import ctypes
+
+import numpy as np
+
+from . import _native
+from .exc import HeartbeatError
+
+
+def hb_encode(obj):
+    """base64 text of bytes, elementwise for lists (util.py:30-34)."""
+    if type(obj) is list:
+        return [hb_encode(x) for x in obj]
+    return base64.b64encode(obj).decode("utf-8")
+
+
+def hb_decode(obj):
+    """Inverse of hb_encode (util.py:37-41)."""
+    if type(obj) is list:
+        return [hb_decode(x) for x in obj]
+    return base64.b64decode(obj.encode("utf-8"))
+
+
+def _key_bytes(key):
+    if isinstance(key, str):
+        key = key.encode("latin-1")
+    return bytes(key)
+
+
+class KeyedPRF(object):
+    """Keyed pseudo random function into [0, range) (util.py:44-96).
+
+    eval(x) = mask & BE(AES-CFB8_key,IV=0(pad(SHA256(str(x)), nb))), with the
+    cipher stream continuing across rejection-sampling tries until the value
+    is < range.  Evaluated on the GPU; ``eval_many`` batches inputs into one
+    kernel launch.
+    """
+
+    @staticmethod
+    def pad(data, length):
+        """Truncate or zero-pad `data` to `length` bytes (util.py:52-64)."""
+        if len(data) > length:
+            return data[0:length]
+        return data + b"\0" * (length - len(data))
+
+    def __init__(self, key, range):
+        self.key = key
+        self.range = range
+        self.mask = (1 << int(range).bit_length()) - 1
+
+    def eval(self, x):
+        return self.eval_many([x])[0]
+
+    def eval_many(self, xs):
+        rng = int(self.range)
+        if rng <= 0:
+            raise HeartbeatError("KeyedPRF range must be positive")
+        xs = [int(x) for x in xs]
+        if any(x < 0 or x >= 1 << 64 for x in xs):
+            raise HeartbeatError("KeyedPRF inputs must be in [0, 2^64)")
+        if not xs:
+            return []
+        key = _key_bytes(self.key)
+        nb = (rng.bit_length() + 7) // 8
+        arr = np.asarray(xs, dtype=np.uint64)
+        out = ctypes.create_string_buffer(nb * len(xs))
+        ctx = _native.context()
+        rb = _native.be(rng)
+        with ctx.lock:
+            ctx.check(_native.lib().hb_prf_eval(ctx.h, key, len(key), rb, len(rb),
+                                                arr.ctypes.data, len(xs), out))
+        raw = out.raw
+        return [int.from_bytes(raw[i * nb:(i + 1) * nb], "big") for i in range(len(xs))]

@@ -1,0 +1,151 @@
+/*
+ * hbswizzle.h -- C ABI of libhbswizzle.so, the MI355X (gfx950) Swizzle
+ * (Shacham-Waters private PDP) hot path.
+ *
+ * The reference has no C ABI: its native boundary is CPython/PyCXX
+ * (cxx/Swizzle.hxx) and pure Python (heartbeat/PySwizzle/PySwizzle.py).  Each
+ * entry point below names the reference interface whose work it replaces.
+ * The Python mirror of the reference API (heartbeat_amd.PySwizzle) binds these
+ * with ctypes; INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *   - Integers crossing the ABI (primes, ranges, tags, mu, sigma) are
+ *     big-endian byte strings, like Crypto.Util.number.long_to_bytes.
+ *   - Tag / proof values are fixed width: hb_width(p) = ceil(bitlen(p)/8)
+ *     bytes each.
+ *   - Buffers are caller-owned.  A pointer flagged *_ON_DEVICE is a device
+ *     pointer on the context's GPU (e.g. a torch.cuda tensor's data_ptr());
+ *     otherwise it is ordinary host memory.  Nothing allocated by the library
+ *     is returned to the caller.
+ *   - Return value 0 = success; negative = error, message in hb_last_error().
+ *     The Python layer raises HeartbeatError(message) (heartbeat/exc.py:29-35).
+ *   - One context per GPU; a context must not be used by two threads at once.
+ *     Calls are synchronous (they return when results are in the caller's
+ *     buffers).
+ *   - There is no CPU fallback: every compute entry point runs HIP kernels and
+ *     fails with an error if no GPU is usable.
+ */
+#ifndef HBSWIZZLE_H
+#define HBSWIZZLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HB_ABI_VERSION 1
+
+/* flags */
+#define HB_DATA_ON_DEVICE 1u   /* `data` is a device pointer */
+#define HB_TAGS_ON_DEVICE 2u   /* `tags` / `tags_out` is a device pointer */
+
+/* error codes */
+#define HB_OK 0
+#define HB_EINVAL -1
+#define HB_EHIP -2
+#define HB_ENOMEM -3
+#define HB_EUNSUPPORTED -4
+
+typedef struct hb_ctx hb_ctx;
+
+int hb_abi_version(void);
+
+/* Open a context on HIP device `device`.  Replaces nothing in the reference
+ * (it runs on the host only); the reference's per-call state lives in
+ * PySwizzle objects (PySwizzle.py:233-255). */
+int hb_ctx_create(int device, hb_ctx **out);
+void hb_ctx_destroy(hb_ctx *ctx);
+/* Message of the last error on this context (or of the last failed
+ * hb_ctx_create when ctx is NULL). */
+const char *hb_last_error(const hb_ctx *ctx);
+
+/* ceil(bitlen(p)/8): width of every tag / mu / sigma value. */
+size_t hb_width(const uint8_t *p_be, size_t p_len);
+
+/* Batched KeyedPRF.eval.
+ * Replaces heartbeat/util.py:83-96 (KeyedPRF.eval) and, for the cxx twin's
+ * callers, cxx/prf.hxx:125-145 (prf::evaluate) -- with PySwizzle semantics.
+ * out[i] = KeyedPRF(key, range).eval(xs[i]), written big-endian with
+ * ceil(bitlen(range)/8) bytes each.  key: 16, 24 or 32 bytes (AES-128/192/256).
+ * xs and out are host buffers. */
+int hb_prf_eval(hb_ctx *ctx, const uint8_t *key, size_t key_len,
+                const uint8_t *range_be, size_t range_len,
+                const uint64_t *xs, size_t n, uint8_t *out);
+
+/* Swizzle encode of a run of blocks.
+ * Replaces heartbeat/PySwizzle/PySwizzle.py:296-309 (the encode loop) and
+ * cxx/shacham_waters_private.cxx:672-697.  For k in [0, nblocks):
+ *   tags[k] = (F(block_base + k) + sum_j alpha(j) * m_kj) mod p
+ * with F = KeyedPRF(f_key, p), alpha = KeyedPRF(alpha_key, p), sector size
+ * ss = bitlen(p)/8, block size C = sectors*ss and m_kj the big-endian integer
+ * of data[k*C + j*ss : min(k*C + (j+1)*ss, len)] (0 when empty; sectors after
+ * the first short one contribute 0, PySwizzle.py:304-306).
+ * A whole-file PySwizzle.encode is block_base = 0, nblocks = len/C + 1
+ * (hb_block_count); shards of a file pass their first block index as
+ * block_base and only their own bytes.
+ * tags: nblocks * hb_width(p) bytes.  *tries_out (may be NULL) receives the
+ * total number of PRF tries spent on the F values (>= nblocks). */
+int hb_encode(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+              const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
+              uint64_t block_base, const uint8_t *data, uint64_t len,
+              uint64_t nblocks, uint8_t *tags, uint32_t flags,
+              uint64_t *tries_out);
+
+/* len/C + 1: the number of tags PySwizzle.encode produces for a file. */
+uint64_t hb_block_count(const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                        uint64_t len);
+
+/* Swizzle prove.
+ * Replaces heartbeat/PySwizzle/PySwizzle.py:333-370 and
+ * cxx/shacham_waters_private.cxx:731-789:
+ *   idx_i = KeyedPRF(chal_key, ntags)(i), v_i = KeyedPRF(chal_key, v_max)(i)
+ *   mu_j  = sum_i v_i * m_{idx_i, j} mod p      (i < chunks)
+ *   sigma = sum_i v_i * tags[idx_i]    mod p
+ * tags: ntags * hb_width(p) bytes.  data: the whole file (len bytes).
+ * mu_out: sectors * hb_width(p) bytes, sigma_out: hb_width(p) bytes (host). */
+int hb_prove(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+             const uint8_t *chal_key, size_t key_len, uint64_t chunks,
+             const uint8_t *vmax_be, size_t vmax_len,
+             const uint8_t *tags, uint64_t ntags,
+             const uint8_t *data, uint64_t len, uint32_t flags,
+             uint8_t *mu_out, uint8_t *sigma_out);
+
+/* Right-hand side of PySwizzle.verify (PySwizzle.py:381-394) for a decrypted
+ * state:  rhs = sum_i v_i * F(idx_i) + sum_j alpha(j) * mu_j  mod p.
+ * The caller compares rhs with proof.sigma.  mu: sectors * hb_width(p) bytes
+ * (each value must be < 2^(8*width)). */
+int hb_verify_rhs(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                  const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
+                  uint64_t state_chunks,
+                  const uint8_t *chal_key, size_t chal_key_len, uint64_t chunks,
+                  const uint8_t *vmax_be, size_t vmax_len,
+                  const uint8_t *mu, uint8_t *rhs_out);
+
+/* Host AES-CFB8 (segment 8, any 16-byte IV) for PySwizzle State
+ * encrypt/decrypt (PySwizzle.py:162-195): 64 bytes per call, not a hot path.
+ * encrypt = 1 encrypts, 0 decrypts. */
+int hb_aes_cfb8(const uint8_t *key, size_t key_len, const uint8_t *iv,
+                const uint8_t *in, uint8_t *out, size_t n, int encrypt);
+
+/* Device timing of the last hb_encode on this context: milliseconds spent in
+ * the encode kernel (HIP events on the kernel's stream), and launch count. */
+int hb_last_kernel_ms(const hb_ctx *ctx, double *ms, uint32_t *launches);
+
+/* Device memory helpers so that callers without a GPU framework (e.g. a cgo or
+ * JNI binding) can hold a device-resident file: allocate, copy
+ * (kind 1 = host->device, 2 = device->host, 3 = device->device), free. */
+int hb_device_malloc(hb_ctx *ctx, uint64_t bytes, void **out);
+int hb_device_free(hb_ctx *ctx, void *ptr);
+int hb_memcpy(hb_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
+
+/* Fill len bytes of device memory with the synthetic SplitMix64 stream used by
+ * the benchmarks and tests: byte k = byte (k mod 8) (little-endian) of
+ * splitmix64(seed ^ (2*(k/16) + ((k mod 16) >= 8)) * 0xD1B54A32D192ED03). */
+int hb_fill_random(hb_ctx *ctx, uint8_t *dev_ptr, uint64_t len, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HBSWIZZLE_H */

@@ -1,0 +1,136 @@
+// CPU emulation of ONE GPU lane of the Swizzle kernels (test tool only).
+//
+// Compiles heartbeat_amd/csrc/hb_lane.hpp as plain C++ and runs the exact lane
+// logic of the encode / PRF kernels sequentially -- same LDS table layout
+// (built for a chosen lane id), same CFB-8 byte-0 AES, same SHA-256 message
+// builder, same Montgomery MAC / reduction -- so it can be compared with the
+// CPU oracle without a GPU (tests/test_emul.py).  Not part of the product.
+#include "../../heartbeat_amd/csrc/hb_lane.hpp"
+#include "../../heartbeat_amd/csrc/hb_aes_host.hpp"
+#include "../../heartbeat_amd/csrc/hb_bignum_host.hpp"
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+using namespace hbhost;
+
+static std::vector<char> g_tab(HB_TAB_BYTES);
+
+static LaneTab make_tab(int lane) {
+    const AesTables &T = aes_tables();
+    for (int e = 0; e < 256; ++e)
+        for (int t = 0; t < 2; ++t)
+            for (int r = 0; r < 32; ++r) {
+                uint32_t v = T.t0[e];
+                if (t) v = (v << 8) | (v >> 24);
+                memcpy(&g_tab[e * 256 + t * 128 + r * 4], &v, 4);
+            }
+    LaneTab L;
+    L.tab = g_tab.data();
+    L.lb0 = (uint32_t)(lane & 31) * 4u;
+    L.lb1 = 128u + (uint32_t)(lane & 31) * 4u;
+    return L;
+}
+
+template <int NL>
+static bool make_prf(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen,
+                     PrfParams<NL> &P, int &nr) {
+    AesKey k;
+    if (!aes_expand(key, keylen, k)) return false;
+    nr = k.nr;
+    memset(&P, 0, sizeof P);
+    memcpy(P.rk, k.rk, sizeof(uint32_t) * 4 * (k.nr + 1));
+    Limbs R = from_be(range_be, rlen, NL);
+    for (int t = 0; t < NL; ++t) P.R[t] = R[t];
+    int bits = bitlen_be(range_be, rlen);
+    P.nb = (uint32_t)(bits + 7) / 8;
+    int top = bits - 8 * ((int)P.nb - 1);
+    P.topmask = (1u << top) - 1u;
+    return bits > 0 && (int)P.nb <= 4 * NL;
+}
+
+template <int NL>
+static int prf_eval(const LaneTab &L, const PrfParams<NL> &P, int nr, uint64_t x, uint32_t out[NL]) {
+    uint32_t dig[8], sr[4] = {0, 0, 0, 0};
+    hb_sha256_decimal(x, dig);
+    for (int tries = 1; tries < 100000; ++tries) {
+        uint32_t ok = 0;
+        if (nr == 10) ok = hb_prf_try<NL, 10>(L, P, sr, dig, out);
+        else if (nr == 12) ok = hb_prf_try<NL, 12>(L, P, sr, dig, out);
+        else ok = hb_prf_try<NL, 14>(L, P, sr, dig, out);
+        if (ok) return tries;
+    }
+    return -1;
+}
+
+template <int NL>
+static int emul_prf_t(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen,
+                      uint64_t x, uint8_t *out_be, int lane) {
+    PrfParams<NL> P;
+    int nr;
+    if (!make_prf<NL>(key, keylen, range_be, rlen, P, nr)) return -1;
+    LaneTab L = make_tab(lane);
+    uint32_t out[NL];
+    int tries = prf_eval<NL>(L, P, nr, x, out);
+    to_be(out, NL, out_be, P.nb);
+    return tries;
+}
+
+extern "C" int emul_prf(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen,
+                        uint64_t x, uint8_t *out_be, int lane) {
+    int bits = bitlen_be(range_be, rlen);
+    if (bits <= 64) return emul_prf_t<2>(key, keylen, range_be, rlen, x, out_be, lane);
+    if (bits <= 256) return emul_prf_t<8>(key, keylen, range_be, rlen, x, out_be, lane);
+    if (bits <= 512) return emul_prf_t<16>(key, keylen, range_be, rlen, x, out_be, lane);
+    if (bits <= 1024) return emul_prf_t<32>(key, keylen, range_be, rlen, x, out_be, lane);
+    return -2;
+}
+
+template <int NL>
+static int emul_encode_t(const uint8_t *p_be, size_t plen, uint32_t S, const uint8_t *fkey,
+                         const uint8_t *akey, size_t keylen, uint64_t block_base,
+                         const uint8_t *data, uint64_t len, uint64_t nblocks, uint8_t *tags, int lane,
+                         int align) {
+    PrfParams<NL> F, A;
+    int nrf, nra;
+    if (!make_prf<NL>(fkey, keylen, p_be, plen, F, nrf)) return -1;
+    if (!make_prf<NL>(akey, keylen, p_be, plen, A, nra)) return -1;
+    LaneTab L = make_tab(lane);
+    Limbs p = from_be(p_be, plen, NL);
+    ModP<NL> M;
+    memset(&M, 0, sizeof M);
+    for (int t = 0; t < NL; ++t) M.p[t] = p[t];
+    M.pinv = mont_pinv(p[0]);
+    M.inv_scaled = inv_scaled(p);
+    Limbs r2 = pow2_mod(64u * NL, p);
+    std::vector<uint32_t> alpha_mont((size_t)S * NL);
+    for (uint32_t j = 0; j < S; ++j) {
+        uint32_t a[NL];
+        prf_eval<NL>(L, A, nra, j, a);
+        hb_to_mont<NL>(a, r2.data(), M, &alpha_mont[(size_t)j * NL]);
+    }
+    int bits = bitlen_be(p_be, plen);
+    uint32_t ss = (uint32_t)bits / 8, tw = (uint32_t)(bits + 7) / 8;
+    uint64_t C = (uint64_t)ss * S;
+    for (uint64_t b = 0; b < nblocks; ++b) {
+        uint32_t f[NL], tag[NL];
+        prf_eval<NL>(L, F, nrf, block_base + b, f);
+        if (align == 16)
+            hb_block_tag<NL, 16>(data, len, b, C, ss, S, alpha_mont.data(), M, f, tag);
+        else
+            hb_block_tag<NL, 1>(data, len, b, C, ss, S, alpha_mont.data(), M, f, tag);
+        hb_store_be<NL>(tags + b * tw, tw, tag);
+    }
+    return 0;
+}
+
+extern "C" int emul_encode(const uint8_t *p_be, size_t plen, uint32_t S, const uint8_t *fkey,
+                           const uint8_t *akey, size_t keylen, uint64_t block_base,
+                           const uint8_t *data, uint64_t len, uint64_t nblocks, uint8_t *tags,
+                           int lane, int align) {
+    int bits = bitlen_be(p_be, plen);
+    if (bits <= 256) return emul_encode_t<8>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align);
+    if (bits <= 512) return emul_encode_t<16>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align);
+    if (bits <= 1024) return emul_encode_t<32>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align);
+    return -2;
+}

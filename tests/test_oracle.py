@@ -1,0 +1,69 @@
+"""The CPU oracle (oracle/swizzle_oracle.c) against golden vectors produced by
+the reference PySwizzle (tests/golden/make_golden.py).  Pins the oracle."""
+import hashlib
+
+from conftest import fixture_file
+
+
+def test_prf_kats(oracle, golden_prf):
+    n = 0
+    for c in golden_prf["cases"]:
+        key = bytes.fromhex(c["key"])
+        rng = int(c["range"])
+        for x, o in zip(c["xs"], c["outs"]):
+            assert oracle.prf_eval(key, rng, int(x)) == int(o), (c["range"], x)
+            n += 1
+    assert n > 1000
+
+
+def test_encode_prove_verify(oracle, golden_encode):
+    for c in golden_encode["cases"]:
+        p = int(c["prime"], 16)
+        S = c["sectors"]
+        data = bytes.fromhex(c["data"])
+        fk, ak = bytes.fromhex(c["f_key"]), bytes.fromhex(c["alpha_key"])
+        tags = oracle.encode(p, S, fk, ak, data)
+        assert tags == [int(t, 16) for t in c["tags"]], c["name"]
+        for chn, prn in (("chal", "proof"), ("chal2", "proof2")):
+            ch = c[chn]
+            mu, sg = oracle.prove(p, S, bytes.fromhex(ch["key"]), ch["chunks"],
+                                  int(ch["v_max"], 16), tags, data)
+            assert mu == [int(m, 16) for m in c[prn]["mu"]], c["name"]
+            assert sg == int(c[prn]["sigma"], 16), c["name"]
+            assert oracle.verify(p, S, fk, ak, len(tags), bytes.fromhex(ch["key"]), ch["chunks"],
+                                 int(ch["v_max"], 16), mu, sg)
+
+
+def test_multithreaded_encode_matches(oracle, golden_files):
+    for c in golden_files["cases"]:
+        data = fixture_file(c["file"])
+        p = int(c["prime"], 16)
+        w = (p.bit_length() + 7) // 8
+        tags = oracle.encode(p, c["sectors"], bytes.fromhex(c["f_key"]),
+                             bytes.fromhex(c["alpha_key"]), data, nthreads=4)
+        assert len(tags) == c["ntags"]
+        h = hashlib.sha256(b"".join(t.to_bytes(w, "big") for t in tags)).hexdigest()
+        assert h == c["tags_sha256"], c["name"]
+        ch = c["chal"]
+        mu, sg = oracle.prove(p, c["sectors"], bytes.fromhex(ch["key"]), ch["chunks"],
+                              int(ch["v_max"], 16), tags, data)
+        assert sg == int(c["proof"]["sigma"], 16)
+        assert mu == [int(m, 16) for m in c["proof"]["mu"]]
+
+
+def test_block_range_encode_is_a_slice(oracle):
+    """Tags of a block range with block_base == the same blocks of a whole-file run."""
+    p = int("db8709c32591ddc589b5c3c0986f92e0d11205b943c23a7e419e6c35b0256e6b", 16)
+    S = 3
+    C = 32 * S
+    data = bytes(range(256)) * 7 + b"xyz"
+    fk, ak = b"f" * 32, b"a" * 32
+    full = oracle.encode(p, S, fk, ak, data)
+    b0, b1 = 5, 13
+    part = oracle.encode(p, S, fk, ak, data[b0 * C:b1 * C], block_base=b0, nblocks=b1 - b0)
+    assert part == full[b0:b1]
+
+
+def test_test6_regenerates():
+    assert hashlib.sha256(fixture_file("test6.txt")).hexdigest() == \
+        "f07be2d96f37df76af247ea305452706f6558d17a01f04e6550dbfc89c8d7cdd"
