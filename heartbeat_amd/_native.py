@@ -19,6 +19,7 @@ HB_TAGS_ON_DEVICE = 2
 
 _lib = None
 _lib_lock = threading.Lock()
+_ctx_lock = threading.Lock()
 _ctxs = {}
 
 # (name, restype, argtypes) for every symbol of include/hbswizzle.h
@@ -111,7 +112,8 @@ def context(device=None):
     d = default_device() if device is None else int(device)
     c = _ctxs.get(d)
     if c is None:
-        with _lib_lock:
+        lib()
+        with _ctx_lock:
             c = _ctxs.get(d)
             if c is None:
                 c = Context(d)
