@@ -142,6 +142,13 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
 }
 
 // ------------------------------------------------------------------ encode
+// Minimum waves per SIMD requested from the register allocator: 4 (= two
+// 512-thread workgroups, 16 waves per CU, the most the 64 KiB-per-workgroup
+// LDS table allows) for primes up to 256 bits; wider primes keep the
+// compiler's choice (they are not the benchmarked configuration).
+template <int NL>
+struct HbEncodeOcc { static constexpr int v = NL <= 8 ? 4 : 1; };
+
 template <int NL, int ALIGN>
 struct EncodeHandler {
     const EncodeArgs<NL> &A;
@@ -154,7 +161,7 @@ struct EncodeHandler {
 };
 
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HB_ENGINE_WG) void hb_encode_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_kernel(EncodeArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L{(const char *)lds, (threadIdx.x & 31u) * 4u, 128u + (threadIdx.x & 31u) * 4u};
@@ -200,7 +207,7 @@ __device__ __forceinline__ void hb_sector_value(const unsigned char *data, u64 l
     if (pos >= len) {
         for (int t = 0; t < NL; ++t) m[t] = 0;
     } else if (pos + ss <= len) {
-        if (ALIGN == 16) hb_load_be_16<NL>(data, pos, ss, m);
+        if (ALIGN == 16) hb_load_full16<NL>(data, pos, m);
         else hb_load_be_bytes<NL>(data, pos, ss, m);
     } else {
         hb_load_be_bytes<NL>(data, pos, (u32)(len - pos), m);

@@ -21,6 +21,14 @@
 #define HB_HD static inline
 #endif
 
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HB_UNROLL _Pragma("unroll")
+#define HB_NOUNROLL _Pragma("unroll 1")
+#else
+#define HB_UNROLL
+#define HB_NOUNROLL
+#endif
+
 typedef uint32_t u32;
 typedef uint64_t u64;
 
@@ -33,6 +41,7 @@ HB_HD u32 hb_perm(u32 s0, u32 s1, u32 sel) {
     // 12 = 0x00, >= 13 = 0xff (8-11, sign replication, unused here).
     u64 v = ((u64)s0 << 32) | s1;
     u32 r = 0;
+    HB_UNROLL
     for (int i = 0; i < 4; ++i) {
         u32 b = (sel >> (8 * i)) & 0xffu, o;
         if (b < 8) o = (u32)(v >> (8 * b)) & 0xffu;
@@ -104,9 +113,7 @@ HB_HD void hb_aes_round(const LaneTab &L, const u32 *rk, u32 &w0, u32 &w1, u32 &
 template <int NR>
 HB_HD u32 hb_aes_byte0(const LaneTab &L, const u32 *rk, u32 s0, u32 s1, u32 s2, u32 s3) {
     u32 w0 = s0 ^ rk[0], w1 = s1 ^ rk[1], w2 = s2 ^ rk[2], w3 = s3 ^ rk[3];
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
+    HB_UNROLL
     for (int r = 1; r <= NR - 2; ++r) hb_aes_round(L, rk + 4 * r, w0, w1, w2, w3);
     u32 a = hb_t<0>(L, w0, L.lb0), b = hb_t<1>(L, w1, L.lb1);
     u32 c = hb_t<2>(L, w2, L.lb0), d = hb_t<3>(L, w3, L.lb1);
@@ -153,9 +160,7 @@ HB_HD void hb_sha256_decimal(u64 x, u32 H[8]) {
         0xc67178f2u};
     u32 a = 0x6a09e667u, b = 0xbb67ae85u, c = 0x3c6ef372u, d = 0xa54ff53au;
     u32 e = 0x510e527fu, f = 0x9b05688cu, g = 0x1f83d9abu, h = 0x5be0cd19u;
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-#endif
+    HB_UNROLL
     for (int t = 0; t < 64; ++t) {
         u32 w;
         if (t < 16) {
@@ -201,15 +206,19 @@ template <int NL, int NR>
 HB_HD u32 hb_prf_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const u32 dig[8],
                      u32 out[NL]) {
     u32 dq[8];
+    HB_UNROLL
     for (int t = 0; t < 8; ++t) dq[t] = dig[t];
+    HB_UNROLL
     for (int t = 0; t < NL; ++t) out[t] = 0;
     u32 m = P.topmask;
     const u32 nw = P.nb >> 2, tail = P.nb & 3u;
     u32 s0 = sr[0], s1 = sr[1], s2 = sr[2], s3 = sr[3];
+    HB_NOUNROLL
     for (u32 wi = 0; wi <= nw; ++wi) {
         const u32 nbytes = wi < nw ? 4u : tail;
         if (nbytes == 0) break;
         u32 dword = dq[0];
+        HB_UNROLL
         for (int t = 0; t < 7; ++t) dq[t] = dq[t + 1];
         dq[7] = 0;
         u32 word = 0;
@@ -224,10 +233,12 @@ HB_HD u32 hb_prf_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const 
             m = 0xffu;
         }
         if (nbytes == 4) {
+            HB_UNROLL
             for (int t = NL - 1; t > 0; --t) out[t] = out[t - 1];
             out[0] = word;
         } else {
             const u32 sh = 32 - 8 * nbytes;   // shift out left by 8*nbytes bits
+            HB_UNROLL
             for (int t = NL - 1; t > 0; --t) out[t] = hb_alignbit(out[t], out[t - 1], sh);
             out[0] = hb_alignbit(out[0], word << sh, sh);
         }
@@ -235,6 +246,7 @@ HB_HD u32 hb_prf_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const 
     sr[0] = s0; sr[1] = s1; sr[2] = s2; sr[3] = s3;
     // out < R  <=>  out - R borrows
     u32 borrow = 0;
+    HB_UNROLL
     for (int t = 0; t < NL; ++t) {
         u64 d = (u64)out[t] - (u64)P.R[t] - (u64)borrow;
         borrow = (u32)(d >> 63);
@@ -259,11 +271,13 @@ template <int NL>
 HB_HD void hb_mac(u32 acc[2 * NL + 1], const u32 *a, const u32 b[NL]) {
     u64 lo = 0;
     u32 hi = 0;
+    HB_UNROLL
     for (int t = 0; t < 2 * NL - 1; ++t) {
         u64 x = lo + acc[t];
         hi += (u32)(x < lo);
         lo = x;
         const int a0 = t < NL ? 0 : t - NL + 1, a1 = t < NL ? t : NL - 1;
+        HB_UNROLL
         for (int i = a0; i <= a1; ++i) {
             u64 pr = (u64)a[i] * b[t - i];
             u64 y = lo + pr;
@@ -285,9 +299,11 @@ HB_HD void hb_mac(u32 acc[2 * NL + 1], const u32 *a, const u32 b[NL]) {
 template <int NL>
 HB_HD void hb_redc(u32 acc[2 * NL + 1], const ModP<NL> &P, u32 v[NL + 1]) {
     u32 extra = 0;
+    HB_UNROLL
     for (int i = 0; i < NL; ++i) {
         u32 q = acc[i] * P.pinv;
         u64 carry = 0;
+        HB_UNROLL
         for (int b = 0; b < NL; ++b) {
             u64 t = (u64)q * P.p[b] + acc[i + b] + carry;
             acc[i + b] = (u32)t;
@@ -298,6 +314,7 @@ HB_HD void hb_redc(u32 acc[2 * NL + 1], const ModP<NL> &P, u32 v[NL + 1]) {
         extra = (u32)(t >> 32);
     }
     acc[2 * NL] += extra;
+    HB_UNROLL
     for (int t = 0; t <= NL; ++t) v[t] = acc[NL + t];
 }
 
@@ -320,6 +337,7 @@ struct HbScale {
 template <int NL>
 HB_HD void hb_reduce_small(u32 v[NL + 1], const ModP<NL> &P, u32 out[NL]) {
     double vd = 0.0, sc = HbScale<NL, 0>::v;
+    HB_UNROLL
     for (int t = 0; t <= NL; ++t) {
         vd += (double)v[t] * sc;
         sc *= 4294967296.0;
@@ -329,6 +347,7 @@ HB_HD void hb_reduce_small(u32 v[NL + 1], const ModP<NL> &P, u32 out[NL]) {
     if (q) {
         u64 carry = 0;
         u32 borrow = 0;
+        HB_UNROLL
         for (int t = 0; t <= NL; ++t) {
             u64 pr = (u64)q * (t < NL ? P.p[t] : 0u) + carry;
             carry = pr >> 32;
@@ -340,14 +359,17 @@ HB_HD void hb_reduce_small(u32 v[NL + 1], const ModP<NL> &P, u32 out[NL]) {
     for (;;) {   // at most a few iterations
         u32 borrow = 0;
         u32 d[NL + 1];
+        HB_UNROLL
         for (int t = 0; t <= NL; ++t) {
             u64 x = (u64)v[t] - (t < NL ? P.p[t] : 0u) - borrow;
             d[t] = (u32)x;
             borrow = (u32)(x >> 63);
         }
         if (borrow) break;   // v < p
+        HB_UNROLL
         for (int t = 0; t <= NL; ++t) v[t] = d[t];
     }
+    HB_UNROLL
     for (int t = 0; t < NL; ++t) out[t] = v[t];
 }
 
@@ -356,9 +378,11 @@ HB_HD void hb_reduce_small(u32 v[NL + 1], const ModP<NL> &P, u32 out[NL]) {
 // byte by byte: used for tail sectors and unaligned sector sizes.
 template <int NL>
 HB_HD void hb_load_be_bytes(const unsigned char *data, u64 off, u32 r, u32 m[NL]) {
+    HB_UNROLL
     for (int t = 0; t < NL; ++t) m[t] = 0;
     for (u32 k = 0; k < r; ++k) {
         u32 byte = data[off + k];
+        HB_UNROLL
         for (int t = NL - 1; t > 0; --t) m[t] = hb_alignbit(m[t], m[t - 1], 24);
         m[0] = (m[0] << 8) | byte;
     }
@@ -368,6 +392,7 @@ HB_HD void hb_load_be_bytes(const unsigned char *data, u64 off, u32 r, u32 m[NL]
 template <int NL>
 HB_HD void hb_load_be_words(const unsigned char *data, u64 off, u32 ss, u32 m[NL]) {
     const u32 nw = ss >> 2;
+    HB_UNROLL
     for (int t = 0; t < NL; ++t) {
         m[t] = 0;
         if ((u32)t < nw) m[t] = hb_bswap(*(const u32 *)(data + off + ss - 4u * (u32)(t + 1)));
@@ -378,10 +403,13 @@ HB_HD void hb_load_be_words(const unsigned char *data, u64 off, u32 ss, u32 m[NL
 template <int NL>
 HB_HD void hb_store_be(unsigned char *dst, u32 tw, const u32 v[NL]) {
     if ((tw & 3u) == 0) {
+        HB_UNROLL
         for (int t = 0; t < NL; ++t)
             if (4u * (u32)(t + 1) <= tw) *(u32 *)(dst + tw - 4u * (u32)(t + 1)) = hb_bswap(v[t]);
     } else {
+        HB_UNROLL
         for (int t = 0; t < NL; ++t)
+            HB_UNROLL
             for (int b = 0; b < 4; ++b) {
                 u32 pos = 4u * (u32)t + (u32)b;   // byte index from the least significant end
                 if (pos < tw) dst[tw - 1 - pos] = (unsigned char)(v[t] >> (8 * b));
@@ -390,27 +418,31 @@ HB_HD void hb_store_be(unsigned char *dst, u32 tw, const u32 v[NL]) {
 }
 
 // ------------------------------------------------------------------ block tag
-// Sector loads of a whole block: ALIGN = 16 (ss % 16 == 0, C % 16 == 0, data
-// 16-byte aligned: 16-byte loads), anything else: byte loads.
+// Sector loads of a whole block.  ALIGN = 16: full-width sectors (ss == 4 NL,
+// e.g. a 256-bit prime with 32-byte sectors), ss, C and the data base all
+// 16-byte aligned: each sector is NL/4 unconditional 16-byte loads, issued for
+// a batch of HB_GROUP(NL) sectors before any of them is consumed.  Any other
+// shape (ALIGN = 1): byte loads.
 template <int NL>
-HB_HD void hb_load_be_16(const unsigned char *data, u64 off, u32 ss, u32 m[NL]) {
+HB_HD void hb_load_full16(const unsigned char *data, u64 off, u32 m[NL]) {
+    HB_UNROLL
     for (int u = 0; u < NL / 4; ++u) {
-        u32 w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        if (16u * (u32)(u + 1) <= ss) {
-            const u32 *q = (const u32 *)(data + off + ss - 16u * (u32)(u + 1));
+        const u32 *q = (const u32 *)(data + off + 4u * NL - 16u * (u32)(u + 1));
 #if defined(__HIP_DEVICE_COMPILE__)
-            uint4 v = *(const uint4 *)q;
-            w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+        uint4 v = *(const uint4 *)q;
+        const u32 w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
 #else
-            w0 = q[0]; w1 = q[1]; w2 = q[2]; w3 = q[3];
+        const u32 w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
 #endif
-        }
         m[4 * u + 0] = hb_bswap(w3);
         m[4 * u + 1] = hb_bswap(w2);
         m[4 * u + 2] = hb_bswap(w1);
         m[4 * u + 3] = hb_bswap(w0);
     }
 }
+
+template <int NL>
+struct HbGroup { static constexpr int v = NL <= 8 ? 2 : (NL <= 16 ? 2 : 1); };
 
 // tag = (F + sum_j alpha_j m_j) mod p for block `blk` of the call
 // (PySwizzle.py:297-307), with alpha in Montgomery form (alpha_j R mod p):
@@ -424,21 +456,43 @@ template <int NL, int ALIGN>
 HB_HD void hb_block_tag(const unsigned char *data, u64 len, u64 blk, u64 C, u32 ss, u32 S,
                         const u32 *alpha_mont, const ModP<NL> &M, const u32 F[NL], u32 tag[NL]) {
     u32 acc[2 * NL + 1];
+    HB_UNROLL
     for (int t = 0; t < NL; ++t) { acc[t] = 0; acc[NL + t] = F[t]; }
     acc[2 * NL] = 0;
     const u64 base = blk * C;
-    u32 m[NL];
     if (base + C <= len) {
-        for (u32 j = 0; j < S; ++j) {
-            if (ALIGN == 16) hb_load_be_16<NL>(data, base + (u64)j * ss, ss, m);
-            else hb_load_be_bytes<NL>(data, base + (u64)j * ss, ss, m);
-            hb_mac<NL>(acc, alpha_mont + (u64)j * NL, m);
+        if (ALIGN == 16) {
+            constexpr int G = HbGroup<NL>::v;
+            u32 j = 0;
+            HB_NOUNROLL
+            for (; j + G <= S; j += G) {
+                u32 m[G][NL];
+                HB_UNROLL
+                for (int g = 0; g < G; ++g) hb_load_full16<NL>(data, base + (u64)(j + g) * ss, m[g]);
+                HB_UNROLL
+                for (int g = 0; g < G; ++g) hb_mac<NL>(acc, alpha_mont + (u64)(j + g) * NL, m[g]);
+            }
+            HB_NOUNROLL
+            for (; j < S; ++j) {
+                u32 m[NL];
+                hb_load_full16<NL>(data, base + (u64)j * ss, m);
+                hb_mac<NL>(acc, alpha_mont + (u64)j * NL, m);
+            }
+        } else {
+            HB_NOUNROLL
+            for (u32 j = 0; j < S; ++j) {
+                u32 m[NL];
+                hb_load_be_bytes<NL>(data, base + (u64)j * ss, ss, m);
+                hb_mac<NL>(acc, alpha_mont + (u64)j * NL, m);
+            }
         }
     } else {
+        HB_NOUNROLL
         for (u32 j = 0; j < S; ++j) {
             const u64 off = base + (u64)j * ss;
             if (off >= len) break;
             const u32 r = (u32)(len - off < ss ? len - off : ss);
+            u32 m[NL];
             hb_load_be_bytes<NL>(data, off, r, m);
             hb_mac<NL>(acc, alpha_mont + (u64)j * NL, m);
             if (r != ss) break;
@@ -453,6 +507,7 @@ HB_HD void hb_block_tag(const unsigned char *data, u64 len, u64 blk, u64 C, u32 
 template <int NL>
 HB_HD void hb_to_mont(const u32 x[NL], const u32 *r2, const ModP<NL> &M, u32 out[NL]) {
     u32 acc[2 * NL + 1];
+    HB_UNROLL
     for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
     hb_mac<NL>(acc, r2, x);
     u32 v[NL + 1];

@@ -193,6 +193,12 @@ int parse_prime(hb_ctx *c, const uint8_t *p_be, size_t p_len, PrimeInfo &pi) {
     return 0;
 }
 
+// Sectors are full limb width and every sector start is 16-byte aligned:
+// the kernels' batched 16-byte load path (hb_lane.hpp, ALIGN = 16).
+bool full16(const PrimeInfo &pi, int nl, u64 C, const void *base) {
+    return pi.ss == 4u * (u32)nl && pi.ss % 16 == 0 && C % 16 == 0 && ((uintptr_t)base % 16) == 0;
+}
+
 // ------------------------------------------------------------------ encode
 template <int NL>
 int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
@@ -237,7 +243,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         A.nblocks = nb;
         A.block_base = base;
         A.tags = tg;
-        const int align = (pi.ss % 16 == 0 && C % 16 == 0 && ((uintptr_t)d % 16) == 0) ? 16 : 1;
+        const int align = full16(pi, NL, C, d) ? 16 : 1;
         // queue[0] is the per-launch job counter; queue[1] accumulates tries
         HB_CHECK(hipMemsetAsync(c->queue, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
         HB_CHECK(hb_launch_encode<NL>(A, nr, align, engine_grid(c, nb), c->stream), "hb_encode_kernel launch");
@@ -372,7 +378,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         A.data = data;
         A.len = len;
         A.tags = tags;
-        align = (pi.ss % 16 == 0 && C % 16 == 0 && ((uintptr_t)data % 16) == 0) ? 16 : 1;
+        align = full16(pi, NL, C, data) ? 16 : 1;
     } else {
         // Gather the challenged blocks (and their tags) on the host -- the
         // reference's file.seek/read per index (PySwizzle.py:353-355) -- and
@@ -423,7 +429,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         HB_CHECK(c->xs.ensure((size_t)chunks * 8), "hipMalloc");
         HB_CHECK(hipMemcpyAsync(c->xs.p, iota.data(), (size_t)chunks * 8, hipMemcpyHostToDevice, c->stream), "H2D");
         A.idx = (const u64 *)c->xs.p;
-        align = (pi.ss % 16 == 0 && C % 16 == 0) ? 16 : 1;
+        align = full16(pi, NL, C, (const uint8_t *)c->data[0].p) ? 16 : 1;
         HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");
         std::vector<uint8_t> out((size_t)ncols * pi.tw);
         rc = finish_sums<NL>(c, p, ncols, nparts, pi.tw, out.data());
