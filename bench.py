@@ -93,16 +93,18 @@ def main():
     ss, w = 32, 32
     C = ss * S
     if args.gib is not None:
-        per_rank = int(args.gib * GIB)
+        file_len = int(args.gib * GIB) * world
     elif cfg["weak"]:
-        per_rank = cfg["gib_per_rank"] * GIB
+        file_len = cfg["gib_per_rank"] * GIB * world
     else:
-        per_rank = cfg["gib_total"] * GIB // world
-    blocks_per_rank = per_rank // C
-    global_blocks = blocks_per_rank * world + 1      # whole-file tag count (trailing empty block)
-    b0 = rank * blocks_per_rank
-    nblocks = blocks_per_rank + (1 if rank == world - 1 else 0)
-    length = blocks_per_rank * C                     # this rank's bytes
+        file_len = cfg["gib_total"] * GIB
+    # rank r encodes its block range of one file of file_len bytes
+    from heartbeat_amd.shard import shard_plan
+    plan = shard_plan(file_len, C, rank, world)
+    global_blocks = plan["total_blocks"]
+    b0 = plan["b0"]
+    nblocks = plan["nblocks"]
+    length = plan["byte_len"]                        # this rank's bytes
 
     fk = hashlib.sha256(b"hb-bench-f").digest()
     ak = hashlib.sha256(b"hb-bench-alpha").digest()
@@ -111,7 +113,7 @@ def main():
     tptr = ctypes.c_void_p()
     ctx.check(L.hb_device_malloc(ctx.h, length, ctypes.byref(dptr)))
     ctx.check(L.hb_device_malloc(ctx.h, nblocks * w, ctypes.byref(tptr)))
-    # rank r's shard is bytes [b0*C, b0*C + length) of one synthetic file
+    # each rank fills its shard from its own seeded stream (bytes do not affect the work)
     ctx.check(L.hb_fill_random(ctx.h, dptr, length, 0x5EED0000 + 3 + rank))
 
     tries = ctypes.c_uint64()
@@ -140,7 +142,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_bytes = length * world * args.steps
+    total_bytes = file_len * args.steps
     value = total_bytes / GIB / elapsed
     kernel_ms = sum(kms) / len(kms)
     achieved_gbs = length / (kernel_ms * 1e-3) / 1e9
@@ -174,6 +176,7 @@ def main():
         "data": "synthetic (SplitMix64 random file bytes, seeded keys)",
         "config": {
             "workload": cfg["name"],
+            "file_bytes": file_len,
             "file_bytes_per_rank": length,
             "blocks_total": global_blocks,
             "sectors": S,
