@@ -12,7 +12,8 @@ import threading
 from .exc import HeartbeatError
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhbswizzle.so")
+# HB_LIB_PATH selects an alternative build (A/B experiments); default: in-tree
+LIB_PATH = os.environ.get("HB_LIB_PATH") or os.path.join(HERE, "libhbswizzle.so")
 
 HB_DATA_ON_DEVICE = 1
 HB_TAGS_ON_DEVICE = 2

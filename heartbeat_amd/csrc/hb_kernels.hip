@@ -154,9 +154,13 @@ struct EncodeHandler {
     const EncodeArgs<NL> &A;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.block_base + job; }
     __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
+#if defined(HB_EXP_NO_MAC)
+        hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, F);
+#else
         u32 tag[NL];
         hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
         hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, tag);
+#endif
     }
 };
 

@@ -63,6 +63,13 @@ HB_HD u32 hb_alignbit(u32 hi, u32 lo, u32 sh) {
 }
 
 HB_HD u32 hb_rotl16(u32 x) { return hb_alignbit(x, x, 16); }
+HB_HD u32 hb_xor3(u32 a, u32 b, u32 c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // v_bitop3_b32: a ^ b ^ c
+#else
+    return a ^ b ^ c;
+#endif
+}
 HB_HD u32 hb_bswap(u32 x) { return hb_perm(x, x, 0x00010203u); }
 
 // ------------------------------------------------------------------ AES
@@ -101,10 +108,10 @@ HB_HD void hb_aes_round(const LaneTab &L, const u32 *rk, u32 &w0, u32 &w1, u32 &
     u32 c2 = hb_t<2>(L, w0, L.lb0), d2 = hb_t<3>(L, w1, L.lb1);
     u32 a3 = hb_t<0>(L, w3, L.lb0), b3 = hb_t<1>(L, w0, L.lb1);
     u32 c3 = hb_t<2>(L, w1, L.lb0), d3 = hb_t<3>(L, w2, L.lb1);
-    w0 = a0 ^ b0 ^ rk[0] ^ hb_rotl16(c0 ^ d0);
-    w1 = a1 ^ b1 ^ rk[1] ^ hb_rotl16(c1 ^ d1);
-    w2 = a2 ^ b2 ^ rk[2] ^ hb_rotl16(c2 ^ d2);
-    w3 = a3 ^ b3 ^ rk[3] ^ hb_rotl16(c3 ^ d3);
+    w0 = hb_xor3(a0, b0, rk[0]) ^ hb_rotl16(c0 ^ d0);
+    w1 = hb_xor3(a1, b1, rk[1]) ^ hb_rotl16(c1 ^ d1);
+    w2 = hb_xor3(a2, b2, rk[2]) ^ hb_rotl16(c2 ^ d2);
+    w3 = hb_xor3(a3, b3, rk[3]) ^ hb_rotl16(c3 ^ d3);
 }
 
 // Byte 0 of AES_k(state).  CFB-8 consumes only that byte, so round NR-1
@@ -267,6 +274,26 @@ struct ModP {
 
 // acc (2NL+1 limbs) += a * b  (a, b: NL limbs).  Product scanning with a
 // 96-bit column accumulator.
+// (hi:lo) += a * b with lo 64-bit, hi 32-bit.  On gfx950 v_mad_u64_u32 has a
+// carry-out, so one product-accumulate is 2 instructions (the generic C form
+// compiles to a 64-bit add + compare + select per product).
+HB_HD void hb_madc(u64 &lo, u32 &hi, u32 a, u32 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    u64 cy;
+    asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
+        "v_addc_co_u32_e64 %1, %2, %1, 0, %2"
+        : "+v"(lo), "+v"(hi), "=&s"(cy)
+        : "v"(a), "v"(b));
+#else
+    u64 pr = (u64)a * b;
+    u64 y = lo + pr;
+    hi += (u32)(y < lo);
+    lo = y;
+#endif
+}
+
+// acc (2NL+1 limbs) += a * b  (a, b: NL limbs).  Product scanning with a
+// 96-bit column accumulator (hi:lo).
 template <int NL>
 HB_HD void hb_mac(u32 acc[2 * NL + 1], const u32 *a, const u32 b[NL]) {
     u64 lo = 0;
@@ -278,12 +305,7 @@ HB_HD void hb_mac(u32 acc[2 * NL + 1], const u32 *a, const u32 b[NL]) {
         lo = x;
         const int a0 = t < NL ? 0 : t - NL + 1, a1 = t < NL ? t : NL - 1;
         HB_UNROLL
-        for (int i = a0; i <= a1; ++i) {
-            u64 pr = (u64)a[i] * b[t - i];
-            u64 y = lo + pr;
-            hi += (u32)(y < lo);
-            lo = y;
-        }
+        for (int i = a0; i <= a1; ++i) hb_madc(lo, hi, a[i], b[t - i]);
         acc[t] = (u32)lo;
         lo = (lo >> 32) | ((u64)hi << 32);
         hi = 0;
@@ -425,6 +447,11 @@ HB_HD void hb_store_be(unsigned char *dst, u32 tw, const u32 v[NL]) {
 // shape (ALIGN = 1): byte loads.
 template <int NL>
 HB_HD void hb_load_full16(const unsigned char *data, u64 off, u32 m[NL]) {
+#if defined(HB_EXP_MAC_NOLOAD)
+    HB_UNROLL
+    for (int t = 0; t < NL; ++t) m[t] = (u32)off * 2654435761u + (u32)t;
+    return;
+#endif
     HB_UNROLL
     for (int u = 0; u < NL / 4; ++u) {
         const u32 *q = (const u32 *)(data + off + 4u * NL - 16u * (u32)(u + 1));
