@@ -4,9 +4,12 @@
 #pragma once
 #include "hb_lane.hpp"
 
-// Workgroup geometry of the PRF engine kernels: 512 threads (8 waves) and a
-// 64 KiB LDS T-table image per workgroup -> 2 workgroups (16 waves) per CU.
-#define HB_ENGINE_WG 512
+// Workgroup geometry of the PRF engine kernels: 1024 threads (16 waves) and a
+// 128 KiB LDS T-table image per workgroup -> 1 workgroup (16 waves) per CU.
+#ifndef HB_ENGINE_WG
+#define HB_ENGINE_WG 1024
+#endif
+#define HB_ENGINE_WG_PER_CU 1
 #define HB_QUEUE_CHUNK 256
 // PRF tries after which a job is abandoned and reported (see hb_engine)
 #define HB_MAX_TRIES 2048u

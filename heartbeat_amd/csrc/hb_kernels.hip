@@ -27,16 +27,22 @@
 
 #define HB_LDS_WORDS (HB_TAB_BYTES / 4)
 
-// Expand the 256-entry global T0 into the replicated LDS image.
+// Expand the 256-entry global T0 into the replicated LDS image (hb_lane.hpp).
 __device__ __forceinline__ void hb_fill_lds(u32 *lds, const u32 *t0) {
-    // 16-byte writes: word group g covers words 4g..4g+3 = same (entry, table)
+    // 16-byte writes: group g covers bytes 16g..16g+15 = one (table, entry)
     for (u32 g = threadIdx.x; g < HB_LDS_WORDS / 4; g += blockDim.x) {
-        const u32 e = g >> 4, t = (g >> 3) & 1u;
+        const u32 off = g * 16u;
+        const u32 e = (off >> 8) & 0xffu, t = ((off >> 16) << 1) | ((off >> 7) & 1u);
         u32 v = t0[e];
-        if (t) v = (v << 8) | (v >> 24);
+        if (t) v = (v << (8 * t)) | (v >> (32 - 8 * t));
         reinterpret_cast<uint4 *>(lds)[g] = make_uint4(v, v, v, v);
     }
     __syncthreads();
+}
+
+__device__ __forceinline__ LaneTab hb_lane_tab(const u32 *lds) {
+    const u32 r4 = (threadIdx.x & 31u) * 4u;
+    return LaneTab{(const char *)lds, {r4, 128u + r4, 0x10000u | r4, 0x10000u | (128u + r4)}};
 }
 
 __device__ __forceinline__ u32 hb_lane_id() { return threadIdx.x & 63u; }
@@ -142,12 +148,16 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
 }
 
 // ------------------------------------------------------------------ encode
-// Minimum waves per SIMD requested from the register allocator: 4 (= two
-// 512-thread workgroups, 16 waves per CU, the most the 64 KiB-per-workgroup
-// LDS table allows) for primes up to 256 bits; wider primes keep the
-// compiler's choice (they are not the benchmarked configuration).
+// Minimum waves per SIMD requested from the register allocator: 4 (= one
+// 1024-thread workgroup, 16 waves per CU, sharing one 128 KiB LDS table
+// image) for primes up to 256 bits; wider primes keep the compiler's choice
+// (they are not the benchmarked configuration).
 template <int NL>
-struct HbEncodeOcc { static constexpr int v = NL <= 8 ? 4 : 1; };
+#ifndef HB_OCC8
+#define HB_OCC8 4
+#endif
+struct HbEncodeOcc { static constexpr int v = NL <= 8 ? HB_OCC8 : 1; };
+
 
 template <int NL, int ALIGN>
 struct EncodeHandler {
@@ -168,7 +178,7 @@ template <int NL, int NR, int ALIGN>
 __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_kernel(EncodeArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
-    const LaneTab L{(const char *)lds, (threadIdx.x & 31u) * 4u, 128u + (threadIdx.x & 31u) * 4u};
+    const LaneTab L = hb_lane_tab(lds);
     EncodeHandler<NL, ALIGN> h{A};
     hb_engine<NL, NR>(h, L, A.prf, A.nblocks, A.queue);
 }
@@ -188,7 +198,7 @@ template <int NL, int NR>
 __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prf_kernel(PrfArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
-    const LaneTab L{(const char *)lds, (threadIdx.x & 31u) * 4u, 128u + (threadIdx.x & 31u) * 4u};
+    const LaneTab L = hb_lane_tab(lds);
     PrfHandler<NL> h{A};
     hb_engine<NL, NR>(h, L, A.prf, A.n, A.queue);
 }

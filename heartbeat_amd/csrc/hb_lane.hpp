@@ -73,45 +73,42 @@ HB_HD u32 hb_xor3(u32 a, u32 b, u32 c) {
 HB_HD u32 hb_bswap(u32 x) { return hb_perm(x, x, 0x00010203u); }
 
 // ------------------------------------------------------------------ AES
-// LDS image of the T tables, 64 KiB: entry e of table t (t = 0: T0, 1: T1 =
-// rotl8(T0)) replica r (0..31) is the u32 at byte
-//     e*256 + t*128 + r*4.
+// LDS image of the four T tables, 128 KiB.  Entry e of table t (Tt =
+// rotl(8t) of T0) replica r (0..31) is the u32 at byte
+//     (t >> 1) * 65536 + e * 256 + (t & 1) * 128 + r * 4.
 // Lane l reads replica (l & 31), so the 32 lanes of each ds_read_b32 half-wave
 // hit 32 distinct banks (bank = (addr/4) mod 32) whatever the indices: no bank
-// conflicts.  The address of T_t[byte k of x] is one v_perm:
-//     {0, 0, x.byte[k], lb_t},  lb_t = t*128 + (lane&31)*4.
-// T2 = rotl16(T0), T3 = rotl16(T1) are applied to the XOR of the T0/T1 pair.
-#define HB_TAB_BYTES 65536
+// conflicts.  The address of Tt[byte k of x] is ONE v_perm_b32:
+//     {0, lb_t.byte2, x.byte[k], lb_t.byte0},  lb_t = (t>>1) << 16 | (t&1)*128 + (l&31)*4.
+// A column of a round is then 4 lookups and two 3-input XORs (v_bitop3).
+#define HB_TAB_BYTES 131072
 
 struct LaneTab {
-    const char *tab;   // LDS image base (generic pointer; LDS after inlining)
-    u32 lb0, lb1;      // lane bases for T0 and T1
+    const char *tab;       // LDS image base (generic pointer; LDS after inlining)
+    u32 lb[4];             // lane bases of T0..T3
 };
 
 HB_HD u32 hb_tab_ld(const char *tab, u32 addr) {
     return *(const u32 *)(tab + addr);
 }
 
-template <int K>
-HB_HD u32 hb_t(const LaneTab &L, u32 x, u32 lb) {
-    u32 addr = hb_perm(x, lb, 0x0c0c0000u | ((4u + K) << 8));
+template <int K, int T>
+HB_HD u32 hb_t(const LaneTab &L, u32 x) {
+    u32 addr = hb_perm(x, L.lb[T], 0x0c020000u | ((4u + K) << 8));
     return hb_tab_ld(L.tab, addr);
 }
 
-// One full AES round on little-endian column words (byte r of w_c = row r).
+// One full AES round on little-endian column words (byte r of w_c = row r):
+// col_c = T0[w_c.0] ^ T1[w_(c+1).1] ^ T2[w_(c+2).2] ^ T3[w_(c+3).3] ^ rk_c.
 HB_HD void hb_aes_round(const LaneTab &L, const u32 *rk, u32 &w0, u32 &w1, u32 &w2, u32 &w3) {
-    u32 a0 = hb_t<0>(L, w0, L.lb0), b0 = hb_t<1>(L, w1, L.lb1);
-    u32 c0 = hb_t<2>(L, w2, L.lb0), d0 = hb_t<3>(L, w3, L.lb1);
-    u32 a1 = hb_t<0>(L, w1, L.lb0), b1 = hb_t<1>(L, w2, L.lb1);
-    u32 c1 = hb_t<2>(L, w3, L.lb0), d1 = hb_t<3>(L, w0, L.lb1);
-    u32 a2 = hb_t<0>(L, w2, L.lb0), b2 = hb_t<1>(L, w3, L.lb1);
-    u32 c2 = hb_t<2>(L, w0, L.lb0), d2 = hb_t<3>(L, w1, L.lb1);
-    u32 a3 = hb_t<0>(L, w3, L.lb0), b3 = hb_t<1>(L, w0, L.lb1);
-    u32 c3 = hb_t<2>(L, w1, L.lb0), d3 = hb_t<3>(L, w2, L.lb1);
-    w0 = hb_xor3(a0, b0, rk[0]) ^ hb_rotl16(c0 ^ d0);
-    w1 = hb_xor3(a1, b1, rk[1]) ^ hb_rotl16(c1 ^ d1);
-    w2 = hb_xor3(a2, b2, rk[2]) ^ hb_rotl16(c2 ^ d2);
-    w3 = hb_xor3(a3, b3, rk[3]) ^ hb_rotl16(c3 ^ d3);
+    u32 a0 = hb_t<0, 0>(L, w0), b0 = hb_t<1, 1>(L, w1), c0 = hb_t<2, 2>(L, w2), d0 = hb_t<3, 3>(L, w3);
+    u32 a1 = hb_t<0, 0>(L, w1), b1 = hb_t<1, 1>(L, w2), c1 = hb_t<2, 2>(L, w3), d1 = hb_t<3, 3>(L, w0);
+    u32 a2 = hb_t<0, 0>(L, w2), b2 = hb_t<1, 1>(L, w3), c2 = hb_t<2, 2>(L, w0), d2 = hb_t<3, 3>(L, w1);
+    u32 a3 = hb_t<0, 0>(L, w3), b3 = hb_t<1, 1>(L, w0), c3 = hb_t<2, 2>(L, w1), d3 = hb_t<3, 3>(L, w2);
+    w0 = hb_xor3(hb_xor3(a0, b0, c0), d0, rk[0]);
+    w1 = hb_xor3(hb_xor3(a1, b1, c1), d1, rk[1]);
+    w2 = hb_xor3(hb_xor3(a2, b2, c2), d2, rk[2]);
+    w3 = hb_xor3(hb_xor3(a3, b3, c3), d3, rk[3]);
 }
 
 // Byte 0 of AES_k(state).  CFB-8 consumes only that byte, so round NR-1
@@ -122,11 +119,9 @@ HB_HD u32 hb_aes_byte0(const LaneTab &L, const u32 *rk, u32 s0, u32 s1, u32 s2, 
     u32 w0 = s0 ^ rk[0], w1 = s1 ^ rk[1], w2 = s2 ^ rk[2], w3 = s3 ^ rk[3];
     HB_UNROLL
     for (int r = 1; r <= NR - 2; ++r) hb_aes_round(L, rk + 4 * r, w0, w1, w2, w3);
-    u32 a = hb_t<0>(L, w0, L.lb0), b = hb_t<1>(L, w1, L.lb1);
-    u32 c = hb_t<2>(L, w2, L.lb0), d = hb_t<3>(L, w3, L.lb1);
-    u32 t = a ^ b ^ rk[4 * (NR - 1)];
-    u32 s = (t ^ ((c ^ d) >> 16)) & 0xffu;
-    u32 o = hb_t<0>(L, s, L.lb0) >> 8;
+    u32 a = hb_t<0, 0>(L, w0), b = hb_t<1, 1>(L, w1), c = hb_t<2, 2>(L, w2), d = hb_t<3, 3>(L, w3);
+    u32 s = hb_xor3(hb_xor3(a, b, c), d, rk[4 * (NR - 1)]) & 0xffu;
+    u32 o = hb_t<0, 0>(L, s) >> 8;
     return (o ^ rk[4 * NR]) & 0xffu;
 }
 
@@ -469,7 +464,10 @@ HB_HD void hb_load_full16(const unsigned char *data, u64 off, u32 m[NL]) {
 }
 
 template <int NL>
-struct HbGroup { static constexpr int v = NL <= 8 ? 2 : (NL <= 16 ? 2 : 1); };
+#ifndef HB_GROUP8
+#define HB_GROUP8 2
+#endif
+struct HbGroup { static constexpr int v = NL <= 8 ? HB_GROUP8 : (NL <= 16 ? 2 : 1); };
 
 // tag = (F + sum_j alpha_j m_j) mod p for block `blk` of the call
 // (PySwizzle.py:297-307), with alpha in Montgomery form (alpha_j R mod p):

@@ -118,7 +118,7 @@ void make_mod(const Limbs &p, ModP<NL> &M) {
 
 int engine_grid(hb_ctx *c, u64 njobs) {
     u64 g = (njobs + HB_ENGINE_WG - 1) / HB_ENGINE_WG;
-    u64 cap = 2ull * (u64)c->num_cus;
+    u64 cap = (u64)HB_ENGINE_WG_PER_CU * (u64)c->num_cus;
     if (g > cap) g = cap;
     return (int)(g ? g : 1);
 }

@@ -5,7 +5,7 @@
 #include <stdio.h>
 #include <stdint.h>
 
-#define N_ITER 4096
+#define N_ITER 32768
 template <int OP>
 __global__ void k(uint32_t *out, uint32_t seed) {
     uint32_t a[8], b = seed * 2654435761u + threadIdx.x;
@@ -49,9 +49,9 @@ int main() {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     int cus = 256;
-    for (int wps = 1; wps <= 8; wps *= 8) {
+    for (int wps = 1; wps <= 8; wps *= 2) {
         for (int op = 0; op < 8; ++op) {
-            dim3 g(cus), b(256 * wps);
+            dim3 g(cus * (wps > 4 ? wps / 4 : 1)), b(256 * (wps > 4 ? 4 : wps));
             for (int rep = 0; rep < 2; ++rep) {
                 (void)hipEventRecord(e0);
                 switch (op) {

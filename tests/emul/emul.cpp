@@ -19,16 +19,19 @@ static std::vector<char> g_tab(HB_TAB_BYTES);
 static LaneTab make_tab(int lane) {
     const AesTables &T = aes_tables();
     for (int e = 0; e < 256; ++e)
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 4; ++t)
             for (int r = 0; r < 32; ++r) {
                 uint32_t v = T.t0[e];
-                if (t) v = (v << 8) | (v >> 24);
-                memcpy(&g_tab[e * 256 + t * 128 + r * 4], &v, 4);
+                if (t) v = (v << (8 * t)) | (v >> (32 - 8 * t));
+                memcpy(&g_tab[(t >> 1) * 65536 + e * 256 + (t & 1) * 128 + r * 4], &v, 4);
             }
     LaneTab L;
     L.tab = g_tab.data();
-    L.lb0 = (uint32_t)(lane & 31) * 4u;
-    L.lb1 = 128u + (uint32_t)(lane & 31) * 4u;
+    const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
+    L.lb[0] = r4;
+    L.lb[1] = 128u + r4;
+    L.lb[2] = 0x10000u | r4;
+    L.lb[3] = 0x10000u | (128u + r4);
     return L;
 }
 
