@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("HB_LIB_PATH") or os.path.join(HERE, "libhbswizzle.so"
 
 HB_DATA_ON_DEVICE = 1
 HB_TAGS_ON_DEVICE = 2
+HB_ENCODE_SINGLE_PASS = 4
 
 _lib = None
 _lib_lock = threading.Lock()

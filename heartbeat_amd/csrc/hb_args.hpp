@@ -13,8 +13,20 @@
 #define HB_QUEUE_CHUNK 256
 // PRF tries after which a job is abandoned and reported (see hb_engine)
 #define HB_MAX_TRIES 2048u
-// job-queue counters per slot: [0] next job, [1] PRF tries, [2] abandoned jobs
+// job-queue counters per slot: [0] next job, [1] PRF tries, [2] abandoned jobs,
+// [3] (encode first pass) evals pushed to the retry list
 #define HB_QSLOT 4
+// queue slots: 0 encode (first pass / single pass), 1 alpha PRF, 2-3 prove,
+// 4-5 verify, 6 hb_prf_eval, 7 encode retry pass
+#define HB_SLOT_RETRY 7
+
+// An eval whose first try was rejected, left for the retry pass: its block
+// (relative to the launch) and the CFB-8 shift register after that try.
+struct HbRetry {
+    u64 blk;
+    u64 pad_;
+    u32 sr[4];
+};
 
 template <int NL>
 struct EncodeArgs {
@@ -29,7 +41,19 @@ struct EncodeArgs {
     const u32 *t0;                // 256-entry T0 table (global)
     unsigned long long *queue;    // HB_QSLOT counters, see above
     u64 C;
-    u32 tw, ss, S, pad_;
+    u32 tw, ss, S;
+    u32 o0;                       // E_fkey(0^16)[0]: keystream byte 0 of every eval
+    const unsigned char *pfx;     // CFB prefix image (hb_lane.hpp), two-pass encode
+    HbRetry *retry;               // retry list (two-pass encode)
+    unsigned long long *retry_count;
+    u64 retry_cap;
+};
+
+// Prefix image of one PRF key (hb_prefix_kernel).
+struct PrefixArgs {
+    u32 rk[60];
+    const u32 *t0;
+    unsigned char *out;           // HB_PFX_BYTES
 };
 
 template <int NL>

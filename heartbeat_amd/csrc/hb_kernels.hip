@@ -103,7 +103,8 @@ struct HbPool {
 };
 
 // The PRF engine: runs KeyedPRF.eval for every job of the queue and calls
-// h.accept(job, value) once per job with the accepted value.
+// h.accept(job, value) once per job with the accepted value.  h.init(job, sr)
+// sets the CFB-8 shift register a job starts from (zero for a fresh eval).
 template <int NL, int NR, class H>
 __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParams<NL> &P,
                                           u64 njobs, unsigned long long *queue) {
@@ -111,7 +112,10 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
     u64 job = 0;
     bool active = pool.take(__ballot(1), true, job);
     u32 dig[8], sr[4] = {0, 0, 0, 0}, out[NL];
-    if (active) hb_sha256_decimal(h.x_of(job), dig);
+    if (active) {
+        h.init(job, sr);
+        hb_sha256_decimal(h.x_of(job), dig);
+    }
     u32 tries = 0, job_tries = 0, failed = 0;
     while (__ballot(active)) {
         const u32 ok = hb_prf_try<NL, NR>(L, P, sr, dig, out);
@@ -133,8 +137,10 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
                 active = got;
                 job = nj;
                 job_tries = 0;
-                sr[0] = sr[1] = sr[2] = sr[3] = 0;   // fresh cipher per eval (util.py:88)
-                if (got) hb_sha256_decimal(h.x_of(job), dig);
+                if (got) {
+                    h.init(job, sr);   // fresh cipher per eval (util.py:88) or a resumed stream
+                    hb_sha256_decimal(h.x_of(job), dig);
+                }
             }
         }
     }
@@ -159,10 +165,13 @@ template <int NL>
 struct HbEncodeOcc { static constexpr int v = NL <= 8 ? HB_OCC8 : 1; };
 
 
+__device__ __forceinline__ void hb_zero_sr(u32 sr[4]) { sr[0] = sr[1] = sr[2] = sr[3] = 0; }
+
 template <int NL, int ALIGN>
 struct EncodeHandler {
     const EncodeArgs<NL> &A;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.block_base + job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
     __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
 #if defined(HB_EXP_NO_MAC)
         hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, F);
@@ -183,11 +192,119 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_ke
     hb_engine<NL, NR>(h, L, A.prf, A.nblocks, A.queue);
 }
 
+// ------------------------------------------------------------------ two-pass encode
+// The prefix image (hb_lane.hpp) turns the first 4 of the nb AES of a fresh
+// eval into three byte loads, but only for a FIRST try: a lane re-dealt in the
+// single-pass engine would still run in lockstep with lanes on later tries.
+// So the encode splits by try:
+//   pass 1 (hb_encode_first_kernel): every lane runs the first try of a fresh
+//          block (nb - 4 AES); accepted blocks are tagged at once, rejected
+//          ones (1 - p/2^bitlen(p) of them, 14 % for the bench prime) are
+//          appended to the retry list with their shift register;
+//   pass 2 (hb_encode_retry_kernel): the single-pass engine over the retry
+//          list, resuming each stream where pass 1 left it.
+// AES per block: nb (E[tries] - 1) + nb - 4 instead of nb E[tries].
+template <int NR>
+__global__ __launch_bounds__(HB_ENGINE_WG) void hb_prefix_kernel(PrefixArgs A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L = hb_lane_tab(lds);
+    const u32 stride = gridDim.x * blockDim.x;
+    for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < HB_PFX_BYTES; i += stride)
+        A.out[i] = (unsigned char)hb_aes_byte0<NR>(L, A.rk, 0u, 0u, 0u, hb_pfx_s3(i));
+}
+
+template <int NL, int NR, int ALIGN>
+__global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L = hb_lane_tab(lds);
+    EncodeHandler<NL, ALIGN> h{A};
+    HbPool pool{0, 0, A.nblocks, A.queue, false};
+    u32 tries = 0, failed = 0;
+    for (;;) {
+        u64 job = 0;
+        const bool active = pool.take(__ballot(1), true, job);
+        if (!__ballot(active)) break;
+        u32 out[NL], sr[4];
+        u32 ok = 1;
+        if (active) {
+            u32 dig[8];
+            hb_sha256_decimal(A.block_base + job, dig);
+            ok = hb_prf_first_try<NL, NR>(L, A.prf, A.pfx, A.o0, sr, dig, out);
+            ++tries;
+        }
+        const u64 rej = __ballot(active && !ok);
+        if (rej) {
+            u64 base = 0;
+            if (hb_lane_id() == 0) base = atomicAdd(A.retry_count, (unsigned long long)__popcll(rej));
+            base = hb_bcast64(base);
+            if (active && !ok) {
+                const u64 slot = base + hb_mbcnt(rej);
+                if (slot < A.retry_cap) {
+                    HbRetry *e = A.retry + slot;
+                    e->blk = job;
+                    *reinterpret_cast<uint4 *>(e->sr) = make_uint4(sr[0], sr[1], sr[2], sr[3]);
+                } else {
+                    // retry list full (never at its sizing, see hb_runtime.cpp):
+                    // finish this eval in place
+                    u32 dig[8];
+                    hb_sha256_decimal(A.block_base + job, dig);
+                    u32 n = 1;
+                    while (!ok && n < HB_MAX_TRIES) {
+                        ok = hb_prf_try<NL, NR>(L, A.prf, sr, dig, out);
+                        ++n;
+                        ++tries;
+                    }
+                    failed += ok ? 0u : 1u;
+                }
+            }
+        }
+        if (active && ok) h.accept(job, out);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        tries += __shfl_xor(tries, off);
+        failed += __shfl_xor(failed, off);
+    }
+    if (hb_lane_id() == 0 && tries) atomicAdd(A.queue + 1, (unsigned long long)tries);
+    if (hb_lane_id() == 0 && failed) atomicAdd(A.queue + 2, (unsigned long long)failed);
+}
+
+template <int NL, int ALIGN>
+struct RetryHandler {
+    const EncodeArgs<NL> &A;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return A.block_base + A.retry[job].blk; }
+    __device__ __forceinline__ void init(u64 job, u32 sr[4]) const {
+        const uint4 v = *reinterpret_cast<const uint4 *>(A.retry[job].sr);
+        sr[0] = v.x; sr[1] = v.y; sr[2] = v.z; sr[3] = v.w;
+    }
+    __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
+        const u64 blk = A.retry[job].blk;
+        u32 tag[NL];
+        hb_block_tag<NL, ALIGN>(A.data, A.len, blk, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
+        hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, tag);
+    }
+};
+
+template <int NL, int NR, int ALIGN>
+__global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_retry_kernel(EncodeArgs<NL> A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    // pass 1 has completed (stream order): the count is final
+    const u64 cnt = *(volatile unsigned long long *)A.retry_count;
+    const u64 n = cnt < A.retry_cap ? cnt : A.retry_cap;
+    if (n == 0) return;
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L = hb_lane_tab(lds);
+    RetryHandler<NL, ALIGN> h{A};
+    hb_engine<NL, NR>(h, L, A.prf, n, A.queue);
+}
+
 // ------------------------------------------------------------------ PRF batch
 template <int NL>
 struct PrfHandler {
     const PrfArgs<NL> &A;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.xs ? A.xs[job] : A.x0 + job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
     __device__ __forceinline__ void accept(u64 job, const u32 v[NL]) const {
         u32 *o = A.out + job * NL;
         for (int t = 0; t < NL; ++t) o[t] = v[t];
@@ -329,16 +446,28 @@ __global__ __launch_bounds__(256) void hb_fill_kernel(unsigned char *dst, u64 le
 // ------------------------------------------------------------------ launchers
 // Plain C++ entry points for hb_runtime.cpp (explicit instantiation per
 // limb count NL, AES rounds NR and sector alignment class).
+// pass: 0 = single-pass engine, 1 = first tries (prefix image), 2 = retry list
 template <int NL>
-hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int grid, hipStream_t s) {
+hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
-#define HB_ENC(NRV, AL) hipLaunchKernelGGL((hb_encode_kernel<NL, NRV, AL>), g, b, 0, s, A)
-    if (align == 16) {
-        if (nr == 14) HB_ENC(14, 16); else if (nr == 12) HB_ENC(12, 16); else HB_ENC(10, 16);
-    } else {
-        if (nr == 14) HB_ENC(14, 1); else if (nr == 12) HB_ENC(12, 1); else HB_ENC(10, 1);
-    }
+#define HB_ENC(K, NRV, AL) hipLaunchKernelGGL((K<NL, NRV, AL>), g, b, 0, s, A)
+#define HB_ENC_NR(K, AL) \
+    do { if (nr == 14) HB_ENC(K, 14, AL); else if (nr == 12) HB_ENC(K, 12, AL); else HB_ENC(K, 10, AL); } while (0)
+#define HB_ENC_AL(K) do { if (align == 16) HB_ENC_NR(K, 16); else HB_ENC_NR(K, 1); } while (0)
+    if (pass == 1) HB_ENC_AL(hb_encode_first_kernel);
+    else if (pass == 2) HB_ENC_AL(hb_encode_retry_kernel);
+    else HB_ENC_AL(hb_encode_kernel);
+#undef HB_ENC_AL
+#undef HB_ENC_NR
 #undef HB_ENC
+    return hipGetLastError();
+}
+
+hipError_t hb_launch_prefix(const PrefixArgs &A, int nr, int grid, hipStream_t s) {
+    dim3 g(grid), b(HB_ENGINE_WG);
+    if (nr == 14) hipLaunchKernelGGL((hb_prefix_kernel<14>), g, b, 0, s, A);
+    else if (nr == 12) hipLaunchKernelGGL((hb_prefix_kernel<12>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((hb_prefix_kernel<10>), g, b, 0, s, A);
     return hipGetLastError();
 }
 
@@ -382,7 +511,7 @@ hipError_t hb_launch_fill(unsigned char *dst, u64 len, u64 seed, hipStream_t s) 
 }
 
 #define HB_INST(NL)                                                                              \
-    template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, hipStream_t); \
+    template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t); \
     template hipError_t hb_launch_prf<NL>(const PrfArgs<NL> &, int, int, hipStream_t);           \
     template hipError_t hb_launch_mont<NL>(const MontArgs<NL> &, hipStream_t);                   \
     template hipError_t hb_launch_wsum<NL>(const WsumArgs<NL> &, int, int, hipStream_t);         \

@@ -204,19 +204,22 @@ struct PrfParams {
 // register bytes).  dig: SHA-256 digest (big-endian words) -- the padded
 // plaintext is dig bytes then zeros (KeyedPRF.pad).  out = mask & BE(ct).
 // Returns 1 if out < R (accepted).
-template <int NL, int NR>
-HB_HD u32 hb_prf_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const u32 dig[8],
-                     u32 out[NL]) {
+//
+// FIRST = 1: the first output word (keystream bytes 0-3 of a fresh eval) is
+// already in out[0] and sr (hb_prf_prefix); the try continues at byte 4.
+template <int NL, int NR, int FIRST>
+HB_HD u32 hb_prf_try_from(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const u32 dig[8],
+                          u32 out[NL]) {
     u32 dq[8];
     HB_UNROLL
-    for (int t = 0; t < 8; ++t) dq[t] = dig[t];
+    for (int t = 0; t < 8; ++t) dq[t] = t + FIRST < 8 ? dig[t + FIRST] : 0u;
     HB_UNROLL
-    for (int t = 0; t < NL; ++t) out[t] = 0;
-    u32 m = P.topmask;
+    for (int t = FIRST; t < NL; ++t) out[t] = 0;
+    u32 m = FIRST ? 0xffu : P.topmask;
     const u32 nw = P.nb >> 2, tail = P.nb & 3u;
     u32 s0 = sr[0], s1 = sr[1], s2 = sr[2], s3 = sr[3];
     HB_NOUNROLL
-    for (u32 wi = 0; wi <= nw; ++wi) {
+    for (u32 wi = FIRST; wi <= nw; ++wi) {
         const u32 nbytes = wi < nw ? 4u : tail;
         if (nbytes == 0) break;
         u32 dword = dq[0];
@@ -254,6 +257,62 @@ HB_HD u32 hb_prf_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const 
         borrow = (u32)(d >> 63);
     }
     return borrow;
+}
+
+template <int NL, int NR>
+HB_HD u32 hb_prf_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const u32 dig[8],
+                     u32 out[NL]) {
+    return hb_prf_try_from<NL, NR, 0>(L, P, sr, dig, out);
+}
+
+// ------------------------------------------------------------------ CFB prefix
+// Every eval starts a fresh cipher with IV = 0 (util.py:88), so the first four
+// AES inputs of the first try are 0^16, 0^15 c0, 0^14 c0 c1 and 0^13 c0 c1 c2:
+// for a fixed key the first four keystream bytes are o0 = E(0)[0] (a
+// constant) and byte 0 of E(...) as a function of the first one, two and three
+// ciphertext bytes.  The prefix image holds those three functions,
+//   P1[c0]                         at HB_PFX_P1 (256 B)
+//   P2[c0 | c1 << 8]               at HB_PFX_P2 (64 KiB)
+//   P3[c0 | c1 << 8 | c2 << 16]    at HB_PFX_P3 (16 MiB),
+// indexed by the register bytes in little-endian order so that the AES input
+// word s3 of an entry is its index shifted left (hb_pfx_s3).  Built once per
+// key (hb_prefix_kernel: 2^24 + 2^16 + 2^8 byte-0 AES, ~0.3 % of a 64 GiB
+// encode); each first try then runs nb - 4 AES instead of nb.
+#define HB_PFX_P1 0u
+#define HB_PFX_P2 256u
+#define HB_PFX_P3 65792u
+#define HB_PFX_BYTES (65792u + (1u << 24))
+
+// AES input word 3 (register bytes 12..15) of prefix image entry i; words 0-2 are 0.
+HB_HD u32 hb_pfx_s3(u32 i) {
+    if (i < HB_PFX_P2) return i << 24;
+    if (i < HB_PFX_P3) return (i - HB_PFX_P2) << 16;
+    return (i - HB_PFX_P3) << 8;
+}
+
+// First four CFB-8 steps of a fresh eval (nb >= 4) from the prefix image:
+// d = digest word 0 (plaintext bytes 0-3, big-endian).  Leaves the shift
+// register in sr and the first output word (top byte masked) in out[0].
+template <int NL>
+HB_HD void hb_prf_prefix(const unsigned char *pfx, u32 o0, const PrfParams<NL> &P, u32 d, u32 sr[4],
+                         u32 out[NL]) {
+    const u32 c0 = ((d >> 24) ^ o0) & 0xffu;
+    const u32 c1 = ((d >> 16) ^ pfx[HB_PFX_P1 + c0]) & 0xffu;
+    u32 x = c0 | (c1 << 8);
+    const u32 c2 = ((d >> 8) ^ pfx[HB_PFX_P2 + x]) & 0xffu;
+    x |= c2 << 16;
+    const u32 c3 = (d ^ pfx[HB_PFX_P3 + x]) & 0xffu;
+    sr[0] = sr[1] = sr[2] = 0;
+    sr[3] = x | (c3 << 24);
+    out[0] = ((c0 & P.topmask) << 24) | (c1 << 16) | (c2 << 8) | c3;
+}
+
+// The first try of a fresh eval through the prefix image (P.nb >= 4).
+template <int NL, int NR>
+HB_HD u32 hb_prf_first_try(const LaneTab &L, const PrfParams<NL> &P, const unsigned char *pfx, u32 o0,
+                           u32 sr[4], const u32 dig[8], u32 out[NL]) {
+    hb_prf_prefix<NL>(pfx, o0, P, dig[0], sr, out);
+    return hb_prf_try_from<NL, NR, 1>(L, P, sr, dig, out);
 }
 
 // ------------------------------------------------------------------ mod p

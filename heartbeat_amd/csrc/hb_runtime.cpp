@@ -8,7 +8,9 @@
 // per-challenge arithmetic runs in the kernels of hb_kernels.hip; there is no
 // CPU compute path.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <string>
 #include <vector>
@@ -21,7 +23,8 @@
 using namespace hbhost;
 
 // launchers (hb_kernels.hip)
-template <int NL> hipError_t hb_launch_encode(const EncodeArgs<NL> &, int, int, int, hipStream_t);
+template <int NL> hipError_t hb_launch_encode(const EncodeArgs<NL> &, int, int, int, int, hipStream_t);
+hipError_t hb_launch_prefix(const PrefixArgs &, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_prf(const PrfArgs<NL> &, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_mont(const MontArgs<NL> &, hipStream_t);
 template <int NL> hipError_t hb_launch_wsum(const WsumArgs<NL> &, int, int, hipStream_t);
@@ -62,6 +65,7 @@ struct hb_ctx {
     u32 *t0 = nullptr;
     unsigned long long *queue = nullptr;   // 16 slots of HB_QSLOT counters
     DevBuf alpha_raw, alpha_mont, xs, vals, vals2, wts, idx, partials, sums, data[2], tags, blen, gtags;
+    DevBuf pfx, retry;   // two-pass encode: CFB prefix image, retry list
     std::string err;
     double last_ms = 0.0;
     u32 last_launches = 0;
@@ -200,6 +204,27 @@ bool full16(const PrimeInfo &pi, int nl, u64 C, const void *base) {
 }
 
 // ------------------------------------------------------------------ encode
+// Retry-list capacity for a launch of nb blocks: the first pass rejects each
+// block with probability q = 1 - p / 2^bitlen(p); room for the mean plus 8
+// standard deviations (a block that finds the list full is finished in place
+// by the first-pass kernel, so the bound only affects speed, never results).
+u64 retry_capacity(const uint8_t *p_be, size_t p_len, u64 nb) {
+    size_t i = 0;
+    while (i < p_len && p_be[i] == 0) ++i;
+    u64 top = 0;
+    size_t k = 0;
+    for (; k < 8 && i + k < p_len; ++k) top = (top << 8) | p_be[i + k];
+    const int rest = 8 * (int)(p_len - i - k);
+    const double frac = ldexp((double)top, rest - bitlen_be(p_be, p_len));
+    double q = 1.0 - frac;
+    if (q < 0) q = 0;
+    const double mean = q * (double)nb;
+    double cap = mean + 8.0 * sqrt(mean) + 1024.0;
+    // test hook: a smaller list, to exercise the in-place overflow path
+    if (const char *t = getenv("HB_TEST_RETRY_CAP")) cap = fmin(cap, atof(t));
+    return cap >= (double)nb ? nb : (u64)cap;
+}
+
 template <int NL>
 int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
                 const uint8_t *f_key, const uint8_t *a_key, size_t key_len, u64 block_base,
@@ -215,18 +240,19 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     if (rc) return rc;
 
     EncodeArgs<NL> A;
+    memset(&A, 0, sizeof A);
     int nr = 0;
     if (!make_prf<NL>(f_key, key_len, p_be, p_len, A.prf, nr)) return fail(c, HB_EINVAL, "invalid key");
     make_mod<NL>(p, A.mod);
     A.alpha_mont = (const u32 *)c->alpha_mont.p;
     A.t0 = c->t0;
-    A.queue = c->queue;
     A.C = C;
     A.tw = pi.tw;
     A.ss = pi.ss;
     A.S = S;
-    A.pad_ = 0;
-    HB_CHECK(hipMemsetAsync(c->queue, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+    unsigned long long *q0 = c->queue, *q7 = c->queue + HB_QSLOT * HB_SLOT_RETRY;
+    HB_CHECK(hipMemsetAsync(q0, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+    HB_CHECK(hipMemsetAsync(q7, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
 
     const bool tags_dev = flags & HB_TAGS_ON_DEVICE;
     uint8_t *dtags = tags;
@@ -234,8 +260,37 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(c->tags.ensure((size_t)(nblocks * pi.tw)), "hipMalloc(tags)");
         dtags = (uint8_t *)c->tags.p;
     }
+    // Host bytes go through the GPU in chunks of cb whole blocks.
+    const bool data_dev = flags & HB_DATA_ON_DEVICE;
+    u64 cb = C ? (256ull << 20) / C : 1;
+    if (cb < 1) cb = 1;
+    const u64 launch_blocks = data_dev ? nblocks : (nblocks < cb ? nblocks : cb);
+    const bool two_pass = A.prf.nb >= 4 && !(flags & HB_ENCODE_SINGLE_PASS);
+    if (two_pass) {
+        HB_CHECK(c->pfx.ensure(HB_PFX_BYTES), "hipMalloc(prefix)");
+        A.retry_cap = retry_capacity(p_be, p_len, launch_blocks);
+        HB_CHECK(c->retry.ensure((size_t)(A.retry_cap ? A.retry_cap : 1) * sizeof(HbRetry)), "hipMalloc(retry)");
+        A.pfx = (const unsigned char *)c->pfx.p;
+        A.retry = (HbRetry *)c->retry.p;
+        A.retry_count = q0 + 3;
+        AesKey k;
+        aes_expand(f_key, key_len, k);
+        uint8_t zero[16] = {0}, o[16];
+        aes_encrypt_block(k, zero, o);
+        A.o0 = o[0];
+    }
     c->last_launches = 0;
     float ms_total = 0.f;
+    // the prefix image is part of the encode (rebuilt for every f_key): timed
+    HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
+    if (two_pass) {
+        PrefixArgs PA;
+        memcpy(PA.rk, A.prf.rk, sizeof PA.rk);
+        PA.t0 = c->t0;
+        PA.out = (unsigned char *)c->pfx.p;
+        HB_CHECK(hb_launch_prefix(PA, nr, c->num_cus, c->stream), "hb_prefix_kernel launch");
+        c->last_launches++;
+    }
 
     auto launch = [&](const uint8_t *d, u64 dlen, u64 nb, u64 base, uint8_t *tg) -> int {
         A.data = d;
@@ -244,15 +299,27 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         A.block_base = base;
         A.tags = tg;
         const int align = full16(pi, NL, C, d) ? 16 : 1;
-        // queue[0] is the per-launch job counter; queue[1] accumulates tries
-        HB_CHECK(hipMemsetAsync(c->queue, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
-        HB_CHECK(hb_launch_encode<NL>(A, nr, align, engine_grid(c, nb), c->stream), "hb_encode_kernel launch");
-        c->last_launches++;
+        // queue[0] is the per-launch job counter (and queue[3] the retry
+        // count); queue[1] accumulates tries
+        HB_CHECK(hipMemsetAsync(q0, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+        if (!two_pass) {
+            A.queue = q0;
+            HB_CHECK(hb_launch_encode<NL>(A, nr, align, 0, engine_grid(c, nb), c->stream), "hb_encode_kernel launch");
+            c->last_launches++;
+            return 0;
+        }
+        HB_CHECK(hipMemsetAsync(q0 + 3, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+        A.queue = q0;
+        HB_CHECK(hb_launch_encode<NL>(A, nr, align, 1, engine_grid(c, nb), c->stream), "hb_encode_first_kernel launch");
+        HB_CHECK(hipMemsetAsync(q7, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+        A.queue = q7;
+        HB_CHECK(hb_launch_encode<NL>(A, nr, align, 2, engine_grid(c, A.retry_cap), c->stream),
+                 "hb_encode_retry_kernel launch");
+        c->last_launches += 2;
         return 0;
     };
 
-    if (flags & HB_DATA_ON_DEVICE) {
-        HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
+    if (data_dev) {
         rc = launch(data, len, nblocks, block_base, dtags);
         if (rc) return rc;
         HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
@@ -260,14 +327,10 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(hipEventElapsedTime(&ms_total, c->k0, c->k1), "hipEventElapsedTime");
     } else {
         // Host bytes: chunks of whole blocks double-buffered through the GPU,
-        // H2D on the copy stream overlapping the encode kernel of the previous
+        // H2D on the copy stream overlapping the encode kernels of the previous
         // chunk on the compute stream.
-        const u64 target = 256ull << 20;
-        u64 cb = C ? target / C : 1;
-        if (cb < 1) cb = 1;
         HB_CHECK(c->data[0].ensure((size_t)(cb * C)), "hipMalloc(staging)");
         HB_CHECK(c->data[1].ensure((size_t)(cb * C)), "hipMalloc(staging)");
-        HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
         for (u64 k0 = 0, it = 0; k0 < nblocks; k0 += cb, ++it) {
             const int b = (int)(it & 1);
             const u64 nb = nblocks - k0 < cb ? nblocks - k0 : cb;
@@ -291,10 +354,11 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     c->last_ms = ms_total;
     if (!tags_dev)
         HB_CHECK(hipMemcpy(tags, dtags, (size_t)(nblocks * pi.tw), hipMemcpyDeviceToHost), "hipMemcpy(tags)");
-    unsigned long long q[HB_QSLOT];
-    HB_CHECK(hipMemcpy(q, c->queue, sizeof q, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
-    if (q[2]) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate for some blocks");
-    if (tries_out) *tries_out = q[1];
+    unsigned long long q[HB_QSLOT], r[HB_QSLOT];
+    HB_CHECK(hipMemcpy(q, q0, sizeof q, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
+    HB_CHECK(hipMemcpy(r, q7, sizeof r, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
+    if (q[2] || r[2]) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate for some blocks");
+    if (tries_out) *tries_out = q[1] + r[1];
     return check_prf_slots(c);
 }
 
@@ -560,7 +624,8 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
-                      &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags};
+                      &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
+                      &c->pfx, &c->retry};
     for (DevBuf *b : bufs) b->release();
     if (c->t0) (void)hipFree(c->t0);
     if (c->queue) (void)hipFree(c->queue);

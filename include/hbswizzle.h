@@ -40,6 +40,9 @@ extern "C" {
 /* flags */
 #define HB_DATA_ON_DEVICE 1u   /* `data` is a device pointer */
 #define HB_TAGS_ON_DEVICE 2u   /* `tags` / `tags_out` is a device pointer */
+#define HB_ENCODE_SINGLE_PASS 4u  /* hb_encode: one-pass engine instead of the
+                                     prefix-image first pass + retry pass (same
+                                     tags; for A/B tests and measurements) */
 
 /* error codes */
 #define HB_OK 0

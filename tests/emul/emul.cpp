@@ -10,6 +10,8 @@
 #include "../../heartbeat_amd/csrc/hb_bignum_host.hpp"
 #include <stdlib.h>
 #include <string.h>
+#include <map>
+#include <string>
 #include <vector>
 
 using namespace hbhost;
@@ -52,13 +54,87 @@ static bool make_prf(const uint8_t *key, size_t keylen, const uint8_t *range_be,
     return bits > 0 && (int)P.nb <= 4 * NL;
 }
 
+// Prefix image of the two-pass encode (hb_lane.hpp, CFB prefix), filled
+// independently of the lane code: P1 and P2 completely and P3 on demand, each
+// entry from the byte-oriented host AES of the register bytes the entry stands
+// for.  Entries of P3 never filled stay 0, so a lane that indexes the image
+// wrongly reads a wrong keystream byte and the tags differ.
+struct Prefix {
+    AesKey k;
+    uint8_t o0 = 0;
+    std::vector<uint8_t> img;
+    std::vector<uint8_t> have3;
+    static uint8_t byte0(const AesKey &k, const uint8_t reg[16]) {
+        uint8_t o[16];
+        aes_encrypt_block(k, reg, o);
+        return o[0];
+    }
+    void init(const uint8_t *key, size_t keylen) {
+        aes_expand(key, keylen, k);
+        img.assign(HB_PFX_BYTES, 0);
+        have3.assign(1u << 24, 0);
+        uint8_t reg[16] = {0};
+        o0 = byte0(k, reg);
+        for (int c0 = 0; c0 < 256; ++c0) {
+            memset(reg, 0, 16);
+            reg[15] = (uint8_t)c0;
+            img[HB_PFX_P1 + c0] = byte0(k, reg);
+            for (int c1 = 0; c1 < 256; ++c1) {
+                memset(reg, 0, 16);
+                reg[14] = (uint8_t)c0;
+                reg[15] = (uint8_t)c1;
+                img[HB_PFX_P2 + (c0 | c1 << 8)] = byte0(k, reg);
+            }
+        }
+    }
+    // make sure the P3 entry the eval of digest word d needs is present
+    void need(uint32_t d) {
+        uint8_t reg[16] = {0};
+        uint8_t c0 = (uint8_t)((d >> 24) ^ o0);
+        reg[15] = c0;
+        uint8_t c1 = (uint8_t)((d >> 16) ^ byte0(k, reg));
+        memset(reg, 0, 16);
+        reg[14] = c0;
+        reg[15] = c1;
+        uint8_t c2 = (uint8_t)((d >> 8) ^ byte0(k, reg));
+        uint32_t ix = (uint32_t)c0 | (uint32_t)c1 << 8 | (uint32_t)c2 << 16;
+        if (have3[ix]) return;
+        memset(reg, 0, 16);
+        reg[13] = c0;
+        reg[14] = c1;
+        reg[15] = c2;
+        img[HB_PFX_P3 + ix] = byte0(k, reg);
+        have3[ix] = 1;
+    }
+};
+
+static Prefix *prefix_for(const uint8_t *key, size_t keylen) {
+    static std::map<std::string, Prefix> cache;
+    std::string kk((const char *)key, keylen);
+    auto it = cache.find(kk);
+    if (it == cache.end()) {
+        it = cache.emplace(kk, Prefix()).first;
+        it->second.init(key, keylen);
+    }
+    return &it->second;
+}
+
+// pfx != NULL: the first try goes through the prefix image (two-pass
+// encode's first pass), later tries resume the stream (retry pass).
 template <int NL>
-static int prf_eval(const LaneTab &L, const PrfParams<NL> &P, int nr, uint64_t x, uint32_t out[NL]) {
+static int prf_eval(const LaneTab &L, const PrfParams<NL> &P, int nr, uint64_t x, uint32_t out[NL],
+                    Prefix *pfx = nullptr) {
     uint32_t dig[8], sr[4] = {0, 0, 0, 0};
     hb_sha256_decimal(x, dig);
     for (int tries = 1; tries < 100000; ++tries) {
         uint32_t ok = 0;
-        if (nr == 10) ok = hb_prf_try<NL, 10>(L, P, sr, dig, out);
+        if (tries == 1 && pfx && P.nb >= 4) {
+            pfx->need(dig[0]);
+            const unsigned char *img = pfx->img.data();
+            if (nr == 10) ok = hb_prf_first_try<NL, 10>(L, P, img, pfx->o0, sr, dig, out);
+            else if (nr == 12) ok = hb_prf_first_try<NL, 12>(L, P, img, pfx->o0, sr, dig, out);
+            else ok = hb_prf_first_try<NL, 14>(L, P, img, pfx->o0, sr, dig, out);
+        } else if (nr == 10) ok = hb_prf_try<NL, 10>(L, P, sr, dig, out);
         else if (nr == 12) ok = hb_prf_try<NL, 12>(L, P, sr, dig, out);
         else ok = hb_prf_try<NL, 14>(L, P, sr, dig, out);
         if (ok) return tries;
@@ -66,26 +142,54 @@ static int prf_eval(const LaneTab &L, const PrfParams<NL> &P, int nr, uint64_t x
     return -1;
 }
 
+// The prefix kernel's entries: byte 0 of the lane AES of (0, 0, 0,
+// hb_pfx_s3(i)) against the host AES, for every P1 / P2 entry and `n3`
+// P3 entries spread over the table.  Returns the number of mismatches.
+extern "C" int emul_prefix_check(const uint8_t *key, size_t keylen, uint32_t n3, int lane) {
+    Prefix ref;
+    ref.init(key, keylen);
+    AesKey k;
+    aes_expand(key, keylen, k);
+    LaneTab L = make_tab(lane);
+    int bad = 0;
+    auto lane_byte = [&](uint32_t i) -> uint8_t {
+        uint32_t s3 = hb_pfx_s3(i);
+        if (k.nr == 10) return (uint8_t)hb_aes_byte0<10>(L, k.rk, 0, 0, 0, s3);
+        if (k.nr == 12) return (uint8_t)hb_aes_byte0<12>(L, k.rk, 0, 0, 0, s3);
+        return (uint8_t)hb_aes_byte0<14>(L, k.rk, 0, 0, 0, s3);
+    };
+    for (uint32_t i = 0; i < HB_PFX_P3; ++i) bad += lane_byte(i) != ref.img[i];
+    for (uint32_t t = 0; t < n3; ++t) {
+        uint32_t ix = (uint32_t)(((uint64_t)t * 2654435761u) & 0xffffffu);
+        uint8_t reg[16] = {0};
+        reg[13] = (uint8_t)ix;
+        reg[14] = (uint8_t)(ix >> 8);
+        reg[15] = (uint8_t)(ix >> 16);
+        bad += lane_byte(HB_PFX_P3 + ix) != Prefix::byte0(k, reg);
+    }
+    return bad;
+}
+
 template <int NL>
 static int emul_prf_t(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen,
-                      uint64_t x, uint8_t *out_be, int lane) {
+                      uint64_t x, uint8_t *out_be, int lane, int use_prefix) {
     PrfParams<NL> P;
     int nr;
     if (!make_prf<NL>(key, keylen, range_be, rlen, P, nr)) return -1;
     LaneTab L = make_tab(lane);
     uint32_t out[NL];
-    int tries = prf_eval<NL>(L, P, nr, x, out);
+    int tries = prf_eval<NL>(L, P, nr, x, out, use_prefix ? prefix_for(key, keylen) : nullptr);
     to_be(out, NL, out_be, P.nb);
     return tries;
 }
 
 extern "C" int emul_prf(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen,
-                        uint64_t x, uint8_t *out_be, int lane) {
+                        uint64_t x, uint8_t *out_be, int lane, int use_prefix) {
     int bits = bitlen_be(range_be, rlen);
-    if (bits <= 64) return emul_prf_t<2>(key, keylen, range_be, rlen, x, out_be, lane);
-    if (bits <= 256) return emul_prf_t<8>(key, keylen, range_be, rlen, x, out_be, lane);
-    if (bits <= 512) return emul_prf_t<16>(key, keylen, range_be, rlen, x, out_be, lane);
-    if (bits <= 1024) return emul_prf_t<32>(key, keylen, range_be, rlen, x, out_be, lane);
+    if (bits <= 64) return emul_prf_t<2>(key, keylen, range_be, rlen, x, out_be, lane, use_prefix);
+    if (bits <= 256) return emul_prf_t<8>(key, keylen, range_be, rlen, x, out_be, lane, use_prefix);
+    if (bits <= 512) return emul_prf_t<16>(key, keylen, range_be, rlen, x, out_be, lane, use_prefix);
+    if (bits <= 1024) return emul_prf_t<32>(key, keylen, range_be, rlen, x, out_be, lane, use_prefix);
     return -2;
 }
 
@@ -93,7 +197,7 @@ template <int NL>
 static int emul_encode_t(const uint8_t *p_be, size_t plen, uint32_t S, const uint8_t *fkey,
                          const uint8_t *akey, size_t keylen, uint64_t block_base,
                          const uint8_t *data, uint64_t len, uint64_t nblocks, uint8_t *tags, int lane,
-                         int align) {
+                         int align, int use_prefix) {
     PrfParams<NL> F, A;
     int nrf, nra;
     if (!make_prf<NL>(fkey, keylen, p_be, plen, F, nrf)) return -1;
@@ -117,7 +221,7 @@ static int emul_encode_t(const uint8_t *p_be, size_t plen, uint32_t S, const uin
     uint64_t C = (uint64_t)ss * S;
     for (uint64_t b = 0; b < nblocks; ++b) {
         uint32_t f[NL], tag[NL];
-        prf_eval<NL>(L, F, nrf, block_base + b, f);
+        prf_eval<NL>(L, F, nrf, block_base + b, f, use_prefix ? prefix_for(fkey, keylen) : nullptr);
         if (align == 16)
             hb_block_tag<NL, 16>(data, len, b, C, ss, S, alpha_mont.data(), M, f, tag);
         else
@@ -130,10 +234,10 @@ static int emul_encode_t(const uint8_t *p_be, size_t plen, uint32_t S, const uin
 extern "C" int emul_encode(const uint8_t *p_be, size_t plen, uint32_t S, const uint8_t *fkey,
                            const uint8_t *akey, size_t keylen, uint64_t block_base,
                            const uint8_t *data, uint64_t len, uint64_t nblocks, uint8_t *tags,
-                           int lane, int align) {
+                           int lane, int align, int use_prefix) {
     int bits = bitlen_be(p_be, plen);
-    if (bits <= 256) return emul_encode_t<8>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align);
-    if (bits <= 512) return emul_encode_t<16>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align);
-    if (bits <= 1024) return emul_encode_t<32>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align);
+    if (bits <= 256) return emul_encode_t<8>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align, use_prefix);
+    if (bits <= 512) return emul_encode_t<16>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align, use_prefix);
+    if (bits <= 1024) return emul_encode_t<32>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align, use_prefix);
     return -2;
 }

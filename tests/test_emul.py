@@ -19,10 +19,11 @@ def emul():
     L = ctypes.CDLL(SO)
     c = ctypes
     L.emul_prf.argtypes = [c.c_char_p, c.c_size_t, c.c_char_p, c.c_size_t, c.c_uint64,
-                           c.c_char_p, c.c_int]
+                           c.c_char_p, c.c_int, c.c_int]
     L.emul_encode.argtypes = [c.c_char_p, c.c_size_t, c.c_uint32, c.c_char_p, c.c_char_p,
                               c.c_size_t, c.c_uint64, c.c_char_p, c.c_uint64, c.c_uint64,
-                              c.c_char_p, c.c_int, c.c_int]
+                              c.c_char_p, c.c_int, c.c_int, c.c_int]
+    L.emul_prefix_check.argtypes = [c.c_char_p, c.c_size_t, c.c_uint32, c.c_int]
     return L
 
 
@@ -30,7 +31,8 @@ def _be(n):
     return n.to_bytes((n.bit_length() + 7) // 8, "big")
 
 
-def test_prf_lane_matches_reference(emul, golden_prf):
+@pytest.mark.parametrize("use_prefix", [0, 1])
+def test_prf_lane_matches_reference(emul, golden_prf, use_prefix):
     lane = 0
     for c in golden_prf["cases"]:
         k = bytes.fromhex(c["key"])
@@ -38,14 +40,14 @@ def test_prf_lane_matches_reference(emul, golden_prf):
         nb = (r.bit_length() + 7) // 8
         for x, o in zip(c["xs"], c["outs"]):
             out = ctypes.create_string_buffer(nb)
-            tries = emul.emul_prf(k, len(k), _be(r), len(_be(r)), int(x), out, lane % 64)
+            tries = emul.emul_prf(k, len(k), _be(r), len(_be(r)), int(x), out, lane % 64, use_prefix)
             lane += 7
             assert tries >= 1
             assert int.from_bytes(out.raw, "big") == int(o), (c["range"], x)
 
 
-@pytest.mark.parametrize("align", [1, 16])
-def test_encode_lane_matches_reference(emul, golden_encode, align):
+@pytest.mark.parametrize("align,use_prefix", [(1, 0), (16, 0), (1, 1), (16, 1)])
+def test_encode_lane_matches_reference(emul, golden_encode, align, use_prefix):
     for c in golden_encode["cases"]:
         p = int(c["prime"], 16)
         bits = p.bit_length()
@@ -58,7 +60,15 @@ def test_encode_lane_matches_reference(emul, golden_encode, align):
         out = ctypes.create_string_buffer(w * nt)
         rc = emul.emul_encode(_be(p), len(_be(p)), c["sectors"], bytes.fromhex(c["f_key"]),
                               bytes.fromhex(c["alpha_key"]), 32, 0, data, len(data), nt, out,
-                              (nt * 13) % 64, align)
+                              (nt * 13) % 64, align, use_prefix)
         assert rc == 0
         got = [int.from_bytes(out.raw[i * w:(i + 1) * w], "big") for i in range(nt)]
         assert got == [int(t, 16) for t in c["tags"]], c["name"]
+
+
+@pytest.mark.parametrize("keylen", [16, 24, 32])
+def test_prefix_image_entries(emul, keylen):
+    """hb_prefix_kernel's entries (lane AES of hb_pfx_s3(i)) == host AES of the
+    register bytes each entry stands for: all of P1, P2 and 4096 P3 entries."""
+    key = bytes(range(7, 7 + keylen))
+    assert emul.emul_prefix_check(key, keylen, 4096, 37) == 0

@@ -277,6 +277,63 @@ def test_device_resident_64mib_vs_oracle(nat, oracle, S, prime_name):
         tb.free()
 
 
+@pytest.mark.parametrize("S,prime_name", [(16, "p256"), (1, "p256"), (5, "p255"), (16, "p256lo"),
+                                          (3, "p1024"), (4, "p61")])
+def test_two_pass_equals_single_pass(nat, S, prime_name):
+    """The two-pass encode (prefix image first pass + retry list) == the
+    single-pass engine (HB_ENCODE_SINGLE_PASS), 16 MiB device-resident; p256lo
+    (2^255 < p) rejects half the first tries."""
+    primes = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))
+    p = int(primes[prime_name], 16)
+    w = nat.width_of(p)
+    L = (16 << 20) + 1000
+    C = (p.bit_length() // 8) * S
+    nb = L // C + 1
+    buf = DevBuf(nat, L)
+    t1 = DevBuf(nat, nb * w)
+    t2 = DevBuf(nat, nb * w)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 4242))
+        fk, ak = hashlib.sha256(b"tp-f").digest(), hashlib.sha256(b"tp-a").digest()
+        pb = nat.be(p)
+        tries = []
+        for flags, tb in ((3, t1), (3 | nat.HB_ENCODE_SINGLE_PASS, t2)):
+            tr = ctypes.c_uint64()
+            ctx.check(nat.lib().hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, buf.p, L, nb, tb.p,
+                                          flags, ctypes.byref(tr)))
+            tries.append(tr.value)
+        assert t1.download() == t2.download()
+        # same PRF streams: the same number of tries either way
+        assert tries[0] == tries[1]
+    finally:
+        buf.free()
+        t1.free()
+        t2.free()
+
+
+def test_two_pass_retry_list_overflow(nat, monkeypatch):
+    """A retry list too small for the rejected first tries: the first pass
+    finishes the overflow in place, tags unchanged."""
+    p = int(json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))["p256lo"], 16)
+    S, L = 4, 4 << 20
+    nb = L // (32 * S) + 1
+    buf = DevBuf(nat, L)
+    t1 = DevBuf(nat, nb * 32)
+    t2 = DevBuf(nat, nb * 32)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 77))
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, t1.p)
+        monkeypatch.setenv("HB_TEST_RETRY_CAP", "1000")
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, t2.p)
+        assert t1.download() == t2.download()
+    finally:
+        buf.free()
+        t1.free()
+        t2.free()
+
+
 def test_shards_concatenate(nat):
     """Block-range shards with awkward boundaries == one whole-file launch."""
     p, S = P256, 16
