@@ -49,6 +49,9 @@ CONFIGS = {
     "c2": dict(name="configs[1]: 1 GiB random file, Swizzle encode, 256-bit prime, "
                     "1 sector/block (per rank for N>1)",
                gib_per_rank=1, sectors=1, weak=True),
+    "c5": dict(name="configs[4]: Swizzle prove() on a 64 GiB device-resident file, 10 000-index "
+                    "challenge, 256-bit prime, 16 sectors/block, 1 MI355X",
+               gib_per_rank=64, sectors=16, weak=True, prove_chunks=10000),
     "c4": dict(name="configs[3]: 256 GiB random file, Swizzle encode, 256-bit prime, "
                     "16 sectors/block, block ranges sharded over N GPUs",
                gib_total=256, sectors=16, weak=False),
@@ -117,6 +120,8 @@ def main():
     ctx.check(L.hb_device_malloc(ctx.h, nblocks * w, ctypes.byref(tptr)))
     # each rank fills its shard from its own seeded stream (bytes do not affect the work)
     ctx.check(L.hb_fill_random(ctx.h, dptr, length, 0x5EED0000 + 3 + rank))
+    if "prove_chunks" in cfg:
+        return bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak, C, rank)
 
     tries = ctypes.c_uint64()
     flags = 3 | (_native.HB_ENCODE_SINGLE_PASS if args.single_pass else 0)
@@ -230,6 +235,69 @@ def main():
         dist.destroy_process_group()
 
 
+def bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak, C, rank):
+    """configs[4]: one step = one PySwizzle.prove (PySwizzle.py:333-370) over
+    the device-resident file and tags: idx / v PRFs for `chunks` indices, the
+    gathered weighted sums of the S sector columns and of the tags, and the
+    mod-p reductions, with mu and sigma copied back to the host."""
+    chunks = cfg["prove_chunks"]
+    ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, dptr, length, nblocks, tptr, 3, None))
+    ck = hashlib.sha256(b"hb-bench-challenge").digest()
+    vb = pb                                   # v_max = p, as gen_challenge (PySwizzle.py:329)
+    w = 32
+    mu = ctypes.create_string_buffer(w * S)
+    sg = ctypes.create_string_buffer(w)
+
+    def step():
+        ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, ck, len(ck), chunks, vb, len(vb), tptr, nblocks,
+                             dptr, length, 3, mu, sg))
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    steps = max(args.steps, 20)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    line = {
+        "metric": "Swizzle prove() latency, ms per proof (device-resident file and tags)",
+        "value": round(ms, 4), "unit": "ms", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": False, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (SplitMix64 random file bytes, seeded keys)",
+        "config": {"workload": cfg["name"], "file_bytes": length, "blocks_total": nblocks,
+                   "sectors": S, "prime_bits": 256, "chunks": chunks},
+        "gathered_bytes_per_proof": chunks * (C + w),
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        import numpy as np
+        from oracle import oracle as O
+        host = np.empty(length, dtype=np.uint8)
+        ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value, length, 2))
+        tags = np.empty(nblocks * w, dtype=np.uint8)
+        ctx.check(L.hb_memcpy(ctx.h, tags.ctypes.data, tptr.value, nblocks * w, 2))
+        t = time.perf_counter()
+        n = 0
+        while n < 3 or time.perf_counter() - t < min(args.cpu_seconds, 5.0):
+            ref_mu = ctypes.create_string_buffer(w * S)
+            ref_sg = ctypes.create_string_buffer(w)
+            rc = O.lib().hbo_prove(pb, len(pb), S, ck, len(ck), chunks, vb, len(vb), nblocks,
+                                   ctypes.cast(tags.ctypes.data, ctypes.c_char_p), w,
+                                   host.ctypes.data, length, ref_mu, ref_sg)
+            if rc:
+                raise RuntimeError("oracle prove error %d" % rc)
+            n += 1
+        cpu_ms = (time.perf_counter() - t) / n * 1e3
+        line["cpu_baseline"] = {"value": round(cpu_ms, 3), "unit": "ms", "cores": 1, "kind": "port",
+                                "sample": "%d proofs of the same challenge, oracle/swizzle_oracle.c "
+                                          "(OpenSSL), 1 thread" % n}
+        line["proof_equal_oracle"] = ref_mu.raw == mu.raw and ref_sg.raw == sg.raw
+        del host, tags
+    print(json.dumps(line), flush=True)
+    ctx.check(L.hb_device_free(ctx.h, dptr))
+    ctx.check(L.hb_device_free(ctx.h, tptr))
+
+
 def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads):
     """Oracle (kind "port") on successive 256 MiB prefixes of the same file
     until `seconds` of CPU work, on `threads` host threads."""
@@ -261,19 +329,40 @@ def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads):
 
 
 def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
-    """Rate with the file in (pageable) host memory: chunked H2D + encode + D2H tags."""
+    """Rate with the file and the tags in host memory (the boundary of a
+    file-like object in, tag bytes out): chunked H2D of sectors + encode + D2H
+    of tags, all inside the timed region, once from a pageable buffer and once
+    from the same buffer page-locked with hb_host_register (pinned DMA)."""
     import numpy as np
     n = min(length, 4 * GIB) // C * C
     host = np.empty(n, dtype=np.uint8)
     ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value, n, 2))
     nb = n // C
     tags = np.empty(nb * 32, dtype=np.uint8)
-    t = time.perf_counter()
-    ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, host.ctypes.data, n, nb,
-                          tags.ctypes.data, 0, None))
-    dt = time.perf_counter() - t
-    return {"value": round(n / GIB / dt, 3), "unit": "GiB/s", "bytes": n,
-            "note": "pageable host buffer, 256 MiB chunks, H2D overlapped with encode"}
+    ref = np.empty(nb * 32, dtype=np.uint8)
+    out = {"bytes": n, "chunk": "256 MiB of whole blocks, double-buffered, H2D / D2H on a copy stream"}
+
+    def run(dst):
+        t = time.perf_counter()
+        ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, host.ctypes.data, n, nb,
+                              dst.ctypes.data, 0, None))
+        return time.perf_counter() - t
+
+    run(ref)   # warm-up (staging buffers, prefix image allocation)
+    out["pageable_gib_s"] = round(n / GIB / run(tags), 3)
+    ok = bool(np.array_equal(tags, ref))
+    ctx.check(L.hb_host_register(ctx.h, host.ctypes.data, n))
+    ctx.check(L.hb_host_register(ctx.h, tags.ctypes.data, tags.nbytes))
+    try:
+        run(tags)
+        out["pinned_gib_s"] = round(n / GIB / run(tags), 3)
+        ok = ok and bool(np.array_equal(tags, ref))
+    finally:
+        ctx.check(L.hb_host_unregister(ctx.h, tags.ctypes.data))
+        ctx.check(L.hb_host_unregister(ctx.h, host.ctypes.data))
+    out["pinned_tags_equal_pageable"] = ok
+    out["unit"] = "GiB/s"
+    return out
 
 
 if __name__ == "__main__":

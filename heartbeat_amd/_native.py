@@ -49,6 +49,8 @@ SIGNATURES = [
     ("hb_device_malloc", _c.c_int, [_P, _c.c_uint64, _c.POINTER(_P)]),
     ("hb_device_free", _c.c_int, [_P, _P]),
     ("hb_memcpy", _c.c_int, [_P, _P, _P, _c.c_uint64, _c.c_int]),
+    ("hb_host_register", _c.c_int, [_P, _P, _c.c_uint64]),
+    ("hb_host_unregister", _c.c_int, [_P, _P]),
     ("hb_fill_random", _c.c_int, [_P, _P, _c.c_uint64, _c.c_uint64]),
 ]
 

@@ -1,0 +1,48 @@
+// Non-template kernels and launchers: prefix image, synthetic data, and the
+// 2-limb PRF used for challenge indices.
+#include "hb_kernels.hpp"
+
+hipError_t hb_launch_prefix(const PrefixArgs &A, int nr, int grid, hipStream_t s) {
+    dim3 g(grid), b(HB_ENGINE_WG);
+    if (nr == 14) hipLaunchKernelGGL((hb_prefix_kernel<14>), g, b, 0, s, A);
+    else if (nr == 12) hipLaunchKernelGGL((hb_prefix_kernel<12>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((hb_prefix_kernel<10>), g, b, 0, s, A);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ synthetic data
+__device__ __forceinline__ u64 hb_splitmix(u64 x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// byte k of the stream = byte (k & 7) (little-endian) of splitmix(seed ^ (k >> 3) * golden)
+__global__ __launch_bounds__(256) void hb_fill_kernel(unsigned char *dst, u64 len, u64 seed) {
+    const u64 nthreads = (u64)gridDim.x * blockDim.x;
+    for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q * 16 < len; q += nthreads) {
+        const u64 a = hb_splitmix(seed ^ ((2 * q) * 0xD1B54A32D192ED03ull));
+        const u64 b = hb_splitmix(seed ^ ((2 * q + 1) * 0xD1B54A32D192ED03ull));
+        if (q * 16 + 16 <= len) {
+            *reinterpret_cast<uint4 *>(dst + q * 16) =
+                make_uint4((u32)a, (u32)(a >> 32), (u32)b, (u32)(b >> 32));
+        } else {
+            for (u64 k = q * 16; k < len; ++k) {
+                const u64 w = (k - q * 16) < 8 ? a : b;
+                dst[k] = (unsigned char)(w >> (8 * ((k - q * 16) & 7)));
+            }
+        }
+    }
+}
+
+hipError_t hb_launch_fill(unsigned char *dst, u64 len, u64 seed, hipStream_t s) {
+    u64 q = (len + 15) / 16;
+    u64 grid = (q + 255) / 256;
+    if (grid > 65536) grid = 65536;
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(hb_fill_kernel, dim3((u32)grid), dim3(256), 0, s, dst, len, seed);
+    return hipGetLastError();
+}
+
+template hipError_t hb_launch_prf<2>(const PrfArgs<2> &, int, int, hipStream_t);

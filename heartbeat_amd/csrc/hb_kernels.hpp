@@ -1,4 +1,5 @@
-// hb_kernels.hip -- CDNA4 (gfx950) kernels of the Swizzle hot path.
+// hb_kernels.hpp -- CDNA4 (gfx950) kernels of the Swizzle hot path (templates;
+// instantiated per limb count by hb_kern_nl*.hip, misc kernels in hb_kern_misc.hip).
 //
 //   hb_encode_kernel   tags of a run of blocks     (PySwizzle.py:296-309)
 //   hb_prf_kernel      batched KeyedPRF.eval        (util.py:83-96)
@@ -22,6 +23,7 @@
 // (hb_lane.hpp, LaneTab): ds_read_b32 lookups are conflict-free for any
 // indices, and the per-CU LDS rate (one wave-wide ds_read_b32 per 2 cycles)
 // is the kernel's binding resource (roofline).
+#pragma once
 #include <hip/hip_runtime.h>
 #include "hb_args.hpp"
 
@@ -214,8 +216,56 @@ __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prefix_kernel(PrefixArgs A) {
         A.out[i] = (unsigned char)hb_aes_byte0<NR>(L, A.rk, 0u, 0u, 0u, hb_pfx_s3(i));
 }
 
+// End of one first try for one job slot of every lane (wave-uniform call):
+// accepted blocks are tagged, rejected ones go to the retry list with their
+// shift register.
+template <int NL, int NR, int ALIGN, class H>
+__device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const LaneTab &L, H &h, u64 job,
+                                                bool active, u32 ok, u32 sr[4], u32 out[NL], u32 &tries,
+                                                u32 &failed) {
+    tries += active ? 1u : 0u;
+    const u64 rej = __ballot(active && !ok);
+    if (rej) {
+        u64 base = 0;
+        if (hb_lane_id() == 0) base = atomicAdd(A.retry_count, (unsigned long long)__popcll(rej));
+        base = hb_bcast64(base);
+        if (active && !ok) {
+            const u64 slot = base + hb_mbcnt(rej);
+            if (slot < A.retry_cap) {
+                HbRetry *e = A.retry + slot;
+                e->blk = job;
+                *reinterpret_cast<uint4 *>(e->sr) = make_uint4(sr[0], sr[1], sr[2], sr[3]);
+            } else {
+                // retry list full (never at its sizing, see hb_runtime.cpp):
+                // finish this eval in place
+                u32 dig[8];
+                hb_sha256_decimal(A.block_base + job, dig);
+                u32 n = 1;
+                while (!ok && n < HB_MAX_TRIES) {
+                    ok = hb_prf_try<NL, NR>(L, A.prf, sr, dig, out);
+                    ++n;
+                    ++tries;
+                }
+                failed += ok ? 0u : 1u;
+            }
+        }
+    }
+    if (active && ok) h.accept(job, out);
+}
+
+// Blocks per lane per first-pass iteration.  Two independent evals whose AES
+// interleave double the ds_read_b32 in flight per round (+11 % LDS lookup rate
+// in isolation, scripts/ubench_aes.hip), but at 128 VGPRs the 256-bit encode
+// spills and measured 933 vs 967 GiB/s at configs[2]: one by default.
+#ifndef HB_FIRST_NJ
+#define HB_FIRST_NJ 1
+#endif
+template <int NL>
+struct HbFirstNJ { static constexpr int v = NL <= 8 ? HB_FIRST_NJ : 1; };
+
 template <int NL, int NR, int ALIGN>
 __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
+    constexpr int NJ = HbFirstNJ<NL>::v;
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
@@ -223,44 +273,26 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
     HbPool pool{0, 0, A.nblocks, A.queue, false};
     u32 tries = 0, failed = 0;
     for (;;) {
-        u64 job = 0;
-        const bool active = pool.take(__ballot(1), true, job);
-        if (!__ballot(active)) break;
-        u32 out[NL], sr[4];
-        u32 ok = 1;
-        if (active) {
-            u32 dig[8];
-            hb_sha256_decimal(A.block_base + job, dig);
-            ok = hb_prf_first_try<NL, NR>(L, A.prf, A.pfx, A.o0, sr, dig, out);
-            ++tries;
-        }
-        const u64 rej = __ballot(active && !ok);
-        if (rej) {
-            u64 base = 0;
-            if (hb_lane_id() == 0) base = atomicAdd(A.retry_count, (unsigned long long)__popcll(rej));
-            base = hb_bcast64(base);
-            if (active && !ok) {
-                const u64 slot = base + hb_mbcnt(rej);
-                if (slot < A.retry_cap) {
-                    HbRetry *e = A.retry + slot;
-                    e->blk = job;
-                    *reinterpret_cast<uint4 *>(e->sr) = make_uint4(sr[0], sr[1], sr[2], sr[3]);
-                } else {
-                    // retry list full (never at its sizing, see hb_runtime.cpp):
-                    // finish this eval in place
-                    u32 dig[8];
-                    hb_sha256_decimal(A.block_base + job, dig);
-                    u32 n = 1;
-                    while (!ok && n < HB_MAX_TRIES) {
-                        ok = hb_prf_try<NL, NR>(L, A.prf, sr, dig, out);
-                        ++n;
-                        ++tries;
-                    }
-                    failed += ok ? 0u : 1u;
-                }
+        u64 job0 = 0, job1 = 0;
+        const bool act0 = pool.take(__ballot(1), true, job0);
+        const bool act1 = NJ == 2 ? pool.take(__ballot(1), true, job1) : false;
+        if (!__ballot(act0 || act1)) break;
+        u32 out[NJ][NL], sr[NJ][4];
+        u32 okm;
+        {
+            u32 dig[NJ][8];
+            hb_sha256_decimal(A.block_base + job0, dig[0]);
+            hb_prf_prefix<NL>(A.pfx, A.o0, A.prf, dig[0][0], sr[0], out[0]);
+            if (NJ == 2) {
+                hb_sha256_decimal(A.block_base + job1, dig[NJ - 1]);
+                hb_prf_prefix<NL>(A.pfx, A.o0, A.prf, dig[NJ - 1][0], sr[NJ - 1], out[NJ - 1]);
             }
+            okm = hb_prf_try_n<NL, NR, 1, NJ>(L, A.prf, sr, dig, out);
         }
-        if (active && ok) h.accept(job, out);
+        hb_first_finish<NL, NR, ALIGN>(A, L, h, job0, act0, okm & 1u, sr[0], out[0], tries, failed);
+        if (NJ == 2)
+            hb_first_finish<NL, NR, ALIGN>(A, L, h, job1, act1, (okm >> 1) & 1u, sr[NJ - 1], out[NJ - 1],
+                                           tries, failed);
     }
     for (int off = 32; off > 0; off >>= 1) {
         tries += __shfl_xor(tries, off);
@@ -417,32 +449,6 @@ __global__ __launch_bounds__(256) void hb_sum_kernel(SumArgs<NL> A) {
     if (threadIdx.x < NL) A.out[col * NL + threadIdx.x] = sh[threadIdx.x];
 }
 
-// ------------------------------------------------------------------ synthetic data
-__device__ __forceinline__ u64 hb_splitmix(u64 x) {
-    x += 0x9E3779B97F4A7C15ull;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-
-// byte k of the stream = byte (k & 7) (little-endian) of splitmix(seed ^ (k >> 3) * golden)
-__global__ __launch_bounds__(256) void hb_fill_kernel(unsigned char *dst, u64 len, u64 seed) {
-    const u64 nthreads = (u64)gridDim.x * blockDim.x;
-    for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q * 16 < len; q += nthreads) {
-        const u64 a = hb_splitmix(seed ^ ((2 * q) * 0xD1B54A32D192ED03ull));
-        const u64 b = hb_splitmix(seed ^ ((2 * q + 1) * 0xD1B54A32D192ED03ull));
-        if (q * 16 + 16 <= len) {
-            *reinterpret_cast<uint4 *>(dst + q * 16) =
-                make_uint4((u32)a, (u32)(a >> 32), (u32)b, (u32)(b >> 32));
-        } else {
-            for (u64 k = q * 16; k < len; ++k) {
-                const u64 w = (k - q * 16) < 8 ? a : b;
-                dst[k] = (unsigned char)(w >> (8 * ((k - q * 16) & 7)));
-            }
-        }
-    }
-}
-
 // ------------------------------------------------------------------ launchers
 // Plain C++ entry points for hb_runtime.cpp (explicit instantiation per
 // limb count NL, AES rounds NR and sector alignment class).
@@ -463,13 +469,6 @@ hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass
     return hipGetLastError();
 }
 
-hipError_t hb_launch_prefix(const PrefixArgs &A, int nr, int grid, hipStream_t s) {
-    dim3 g(grid), b(HB_ENGINE_WG);
-    if (nr == 14) hipLaunchKernelGGL((hb_prefix_kernel<14>), g, b, 0, s, A);
-    else if (nr == 12) hipLaunchKernelGGL((hb_prefix_kernel<12>), g, b, 0, s, A);
-    else hipLaunchKernelGGL((hb_prefix_kernel<10>), g, b, 0, s, A);
-    return hipGetLastError();
-}
 
 template <int NL>
 hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int grid, hipStream_t s) {
@@ -501,22 +500,9 @@ hipError_t hb_launch_sum(const SumArgs<NL> &A, int ncols, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t hb_launch_fill(unsigned char *dst, u64 len, u64 seed, hipStream_t s) {
-    u64 q = (len + 15) / 16;
-    u64 grid = (q + 255) / 256;
-    if (grid > 65536) grid = 65536;
-    if (grid == 0) grid = 1;
-    hipLaunchKernelGGL(hb_fill_kernel, dim3((u32)grid), dim3(256), 0, s, dst, len, seed);
-    return hipGetLastError();
-}
-
 #define HB_INST(NL)                                                                              \
     template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t); \
     template hipError_t hb_launch_prf<NL>(const PrfArgs<NL> &, int, int, hipStream_t);           \
     template hipError_t hb_launch_mont<NL>(const MontArgs<NL> &, hipStream_t);                   \
     template hipError_t hb_launch_wsum<NL>(const WsumArgs<NL> &, int, int, hipStream_t);         \
     template hipError_t hb_launch_sum<NL>(const SumArgs<NL> &, int, hipStream_t);
-HB_INST(8)
-HB_INST(16)
-HB_INST(32)
-template hipError_t hb_launch_prf<2>(const PrfArgs<2> &, int, int, hipStream_t);

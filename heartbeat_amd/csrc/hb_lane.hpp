@@ -125,6 +125,29 @@ HB_HD u32 hb_aes_byte0(const LaneTab &L, const u32 *rk, u32 s0, u32 s1, u32 s2, 
     return (o ^ rk[4 * NR]) & 0xffu;
 }
 
+// hb_aes_byte0 for N independent states at once (s[n][0..3] -> o[n]): the N
+// states' lookups of a round are independent, so a wave keeps up to 16 N
+// ds_read_b32 in flight per round instead of 16.
+template <int NR, int N>
+HB_HD void hb_aes_byte0_n(const LaneTab &L, const u32 *rk, const u32 s[N][4], u32 o[N]) {
+    u32 w[N][4];
+    HB_UNROLL
+    for (int n = 0; n < N; ++n)
+        HB_UNROLL
+        for (int c = 0; c < 4; ++c) w[n][c] = s[n][c] ^ rk[c];
+    HB_UNROLL
+    for (int r = 1; r <= NR - 2; ++r)
+        HB_UNROLL
+        for (int n = 0; n < N; ++n) hb_aes_round(L, rk + 4 * r, w[n][0], w[n][1], w[n][2], w[n][3]);
+    HB_UNROLL
+    for (int n = 0; n < N; ++n) {
+        u32 a = hb_t<0, 0>(L, w[n][0]), b = hb_t<1, 1>(L, w[n][1]), c = hb_t<2, 2>(L, w[n][2]),
+            d = hb_t<3, 3>(L, w[n][3]);
+        u32 x = hb_xor3(hb_xor3(a, b, c), d, rk[4 * (NR - 1)]) & 0xffu;
+        o[n] = ((hb_t<0, 0>(L, x) >> 8) ^ rk[4 * NR]) & 0xffu;
+    }
+}
+
 // ------------------------------------------------------------------ SHA-256
 HB_HD u32 hb_rotr(u32 x, u32 n) { return hb_alignbit(x, x, n); }
 
@@ -305,6 +328,77 @@ HB_HD void hb_prf_prefix(const unsigned char *pfx, u32 o0, const PrfParams<NL> &
     sr[0] = sr[1] = sr[2] = 0;
     sr[3] = x | (c3 << 24);
     out[0] = ((c0 & P.topmask) << 24) | (c1 << 16) | (c2 << 8) | c3;
+}
+
+// hb_prf_try_from for N independent evals of the same PRF in lockstep (all
+// at the same point of a try): the AES of the N streams are interleaved
+// (hb_aes_byte0_n).  Returns bit n set iff stream n's try was accepted.
+template <int NL, int NR, int FIRST, int N>
+HB_HD u32 hb_prf_try_n(const LaneTab &L, const PrfParams<NL> &P, u32 sr[N][4], const u32 dig[N][8],
+                       u32 out[N][NL]) {
+    u32 dq[N][8];
+    HB_UNROLL
+    for (int n = 0; n < N; ++n) {
+        HB_UNROLL
+        for (int t = 0; t < 8; ++t) dq[n][t] = t + FIRST < 8 ? dig[n][t + FIRST] : 0u;
+        HB_UNROLL
+        for (int t = FIRST; t < NL; ++t) out[n][t] = 0;
+    }
+    u32 m = FIRST ? 0xffu : P.topmask;
+    const u32 nw = P.nb >> 2, tail = P.nb & 3u;
+    HB_NOUNROLL
+    for (u32 wi = FIRST; wi <= nw; ++wi) {
+        const u32 nbytes = wi < nw ? 4u : tail;
+        if (nbytes == 0) break;
+        u32 dword[N], word[N];
+        HB_UNROLL
+        for (int n = 0; n < N; ++n) {
+            dword[n] = dq[n][0];
+            HB_UNROLL
+            for (int t = 0; t < 7; ++t) dq[n][t] = dq[n][t + 1];
+            dq[n][7] = 0;
+            word[n] = 0;
+        }
+        for (u32 bi = 0; bi < nbytes; ++bi) {
+            u32 o[N];
+            hb_aes_byte0_n<NR, N>(L, P.rk, sr, o);
+            HB_UNROLL
+            for (int n = 0; n < N; ++n) {
+                const u32 c = ((dword[n] >> (24 - 8 * bi)) & 0xffu) ^ o[n];
+                sr[n][0] = hb_alignbit(sr[n][1], sr[n][0], 8);
+                sr[n][1] = hb_alignbit(sr[n][2], sr[n][1], 8);
+                sr[n][2] = hb_alignbit(sr[n][3], sr[n][2], 8);
+                sr[n][3] = (sr[n][3] >> 8) | (c << 24);
+                word[n] = (word[n] << 8) | (c & m);
+            }
+            m = 0xffu;
+        }
+        HB_UNROLL
+        for (int n = 0; n < N; ++n) {
+            if (nbytes == 4) {
+                HB_UNROLL
+                for (int t = NL - 1; t > 0; --t) out[n][t] = out[n][t - 1];
+                out[n][0] = word[n];
+            } else {
+                const u32 sh = 32 - 8 * nbytes;
+                HB_UNROLL
+                for (int t = NL - 1; t > 0; --t) out[n][t] = hb_alignbit(out[n][t], out[n][t - 1], sh);
+                out[n][0] = hb_alignbit(out[n][0], word[n] << sh, sh);
+            }
+        }
+    }
+    u32 okm = 0;
+    HB_UNROLL
+    for (int n = 0; n < N; ++n) {
+        u32 borrow = 0;
+        HB_UNROLL
+        for (int t = 0; t < NL; ++t) {
+            u64 d = (u64)out[n][t] - (u64)P.R[t] - (u64)borrow;
+            borrow = (u32)(d >> 63);
+        }
+        okm |= borrow << n;
+    }
+    return okm;
 }
 
 // The first try of a fresh eval through the prefix image (P.nb >= 4).

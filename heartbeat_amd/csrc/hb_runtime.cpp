@@ -331,6 +331,14 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         // chunk on the compute stream.
         HB_CHECK(c->data[0].ensure((size_t)(cb * C)), "hipMalloc(staging)");
         HB_CHECK(c->data[1].ensure((size_t)(cb * C)), "hipMalloc(staging)");
+        auto tags_back = [&](u64 k, u64 n, int buf) -> int {
+            HB_CHECK(hipStreamWaitEvent(c->copy, c->done[buf], 0), "hipStreamWaitEvent");
+            HB_CHECK(hipMemcpyAsync(tags + k * pi.tw, dtags + k * pi.tw, (size_t)(n * pi.tw),
+                                    hipMemcpyDeviceToHost, c->copy),
+                     "hipMemcpyAsync(D2H tags)");
+            return 0;
+        };
+        u64 last_k0 = 0, last_nb = 0;
         for (u64 k0 = 0, it = 0; k0 < nblocks; k0 += cb, ++it) {
             const int b = (int)(it & 1);
             const u64 nb = nblocks - k0 < cb ? nblocks - k0 : cb;
@@ -346,13 +354,25 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             rc = launch((const uint8_t *)c->data[b].p, bytes, nb, block_base + k0, dtags + k0 * pi.tw);
             if (rc) return rc;
             HB_CHECK(hipEventRecord(c->done[b], c->stream), "hipEventRecord");
+            // the previous chunk's tags go back on the copy stream behind this
+            // chunk's H2D (which must not wait for the previous encode)
+            if (it >= 1 && !tags_dev) rc = tags_back(k0 - cb, cb, 1 - b);
+            if (rc) return rc;
+            last_k0 = k0;
+            last_nb = nb;
+        }
+        if (!tags_dev && nblocks) rc = tags_back(last_k0, last_nb, (int)(((nblocks - 1) / cb) & 1));
+        if (rc) return rc;
+        if (!tags_dev) {
+            HB_CHECK(hipEventRecord(c->copied[0], c->copy), "hipEventRecord");
+            HB_CHECK(hipStreamWaitEvent(c->stream, c->copied[0], 0), "hipStreamWaitEvent");
         }
         HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
         HB_CHECK(hipEventSynchronize(c->k1), "encode");
         HB_CHECK(hipEventElapsedTime(&ms_total, c->k0, c->k1), "hipEventElapsedTime");
     }
     c->last_ms = ms_total;
-    if (!tags_dev)
+    if (!tags_dev && data_dev)
         HB_CHECK(hipMemcpy(tags, dtags, (size_t)(nblocks * pi.tw), hipMemcpyDeviceToHost), "hipMemcpy(tags)");
     unsigned long long q[HB_QSLOT], r[HB_QSLOT];
     HB_CHECK(hipMemcpy(q, q0, sizeof q, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
@@ -778,6 +798,20 @@ int hb_device_free(hb_ctx *c, void *p) {
     if (!c) return HB_EINVAL;
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     HB_CHECK(hipFree(p), "hipFree");
+    return 0;
+}
+
+int hb_host_register(hb_ctx *c, void *ptr, uint64_t bytes) {
+    if (!c || !ptr || !bytes) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    HB_CHECK(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault), "hipHostRegister");
+    return 0;
+}
+
+int hb_host_unregister(hb_ctx *c, void *ptr) {
+    if (!c || !ptr) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    HB_CHECK(hipHostUnregister(ptr), "hipHostUnregister");
     return 0;
 }
 

@@ -143,6 +143,15 @@ int hb_device_malloc(hb_ctx *ctx, uint64_t bytes, void **out);
 int hb_device_free(hb_ctx *ctx, void *ptr);
 int hb_memcpy(hb_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
 
+/* Page-lock (pin) an existing host buffer for the device of ctx, e.g. the file
+ * bytes and the tag buffer of a host-path hb_encode: pinned chunks are copied
+ * by DMA at the full PCIe rate and overlap the encode of the previous chunk
+ * (pageable ones go through a driver staging copy).  The reference reads the
+ * file through Python read() calls (PySwizzle.py:299; cxx/PythonSeekableFile.hxx:47-54);
+ * this is the native replacement's staging.  Unregister before freeing. */
+int hb_host_register(hb_ctx *ctx, void *ptr, uint64_t bytes);
+int hb_host_unregister(hb_ctx *ctx, void *ptr);
+
 /* Fill len bytes of device memory with the synthetic SplitMix64 stream used by
  * the benchmarks and tests: byte k = byte (k mod 8) (little-endian) of
  * splitmix64(seed ^ (2*(k/16) + ((k mod 16) >= 8)) * 0xD1B54A32D192ED03). */

@@ -14,6 +14,9 @@ if [ -z "$NOTESTS" ]; then
 fi
 step bench_c3 400 python -u bench.py --steps 5 --warmup 1 --cpu-seconds 10 ${HOSTPATH:+--host-path} || exit 1
 step bench_c2 200 python -u bench.py --config c2 --steps 10 --warmup 2 --no-cpu-baseline || exit 1
+if [ -n "$PROVE" ]; then
+  step bench_c5 300 python -u bench.py --config c5 --steps 20 --warmup 2 || exit 1
+fi
 if [ -n "$AB" ]; then
   step bench_c3_single 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --single-pass || exit 1
   step bench_c2_single 200 python -u bench.py --config c2 --steps 10 --warmup 2 --no-cpu-baseline --single-pass || exit 1

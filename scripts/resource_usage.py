@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel VGPR / SGPR / scratch / occupancy of hb_kernels.hip for gfx950
+"""Per-kernel VGPR / SGPR / scratch / occupancy of hb_kern_nl8.hip for gfx950
 (hipcc -Rpass-analysis=kernel-resource-usage), one line per kernel."""
 import re
 import subprocess
@@ -7,7 +7,7 @@ import sys
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-src = os.path.join(ROOT, "heartbeat_amd", "csrc", "hb_kernels.hip")
+src = os.path.join(ROOT, "heartbeat_amd", "csrc", os.environ.get("HB_RU_SRC", "hb_kern_nl8.hip"))
 out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", src,
                       "-o", "/tmp/_ru.o", "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:],
                      capture_output=True, text=True).stderr

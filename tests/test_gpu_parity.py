@@ -380,6 +380,36 @@ def test_host_path_chunks_equal_device_path(nat, pys):
         tb.free()
 
 
+def test_host_path_pinned_equals_device_path(nat):
+    """Pinned (hb_host_register) host file and tag buffers, S = 1 so that the
+    per-chunk tag D2H is as large as the H2D: == device-resident tags."""
+    p, S = P256, 1
+    L = (300 << 20) + 5
+    nb = L // 32 + 1
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * 32)
+    ctx = nat.context()
+    lib = nat.lib()
+    try:
+        ctx.check(lib.hb_fill_random(ctx.h, buf.p, L, 7))
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, tb.p)
+        host = np.frombuffer(buf.download(), dtype=np.uint8).copy()
+        tags = np.zeros(nb * 32, dtype=np.uint8)
+        ctx.check(lib.hb_host_register(ctx.h, host.ctypes.data, host.nbytes))
+        ctx.check(lib.hb_host_register(ctx.h, tags.ctypes.data, tags.nbytes))
+        try:
+            pb = nat.be(p)
+            ctx.check(lib.hb_encode(ctx.h, pb, len(pb), S, b"f" * 32, b"a" * 32, 32, 0,
+                                    host.ctypes.data, L, nb, tags.ctypes.data, 0, None))
+        finally:
+            ctx.check(lib.hb_host_unregister(ctx.h, tags.ctypes.data))
+            ctx.check(lib.hb_host_unregister(ctx.h, host.ctypes.data))
+        assert tags.tobytes() == tb.download()
+    finally:
+        buf.free()
+        tb.free()
+
+
 def test_prove_device_resident_vs_oracle(nat, oracle):
     """Config-5 shape at 64 MiB: 10 000-index challenge, device-resident file and tags."""
     p, S = P256, 16
