@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--single-pass", action="store_true",
                     help="one-pass PRF engine instead of prefix-image first pass + retry pass")
+    ap.add_argument("--prf", default="pyswizzle", choices=["pyswizzle", "cxx"],
+                    help="pyswizzle: KeyedPRF, tags bit-exact vs PySwizzle (the headline); cxx: the "
+                         "cxx Swizzle extension's PRF (cxx/prf.hxx, CFB-128), parity unpinned")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the pinned/pageable host path on a 4 GiB prefix (DESIGN.md)")
     return ap.parse_args()
@@ -124,7 +127,8 @@ def main():
         return bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak, C, rank)
 
     tries = ctypes.c_uint64()
-    flags = 3 | (_native.HB_ENCODE_SINGLE_PASS if args.single_pass else 0)
+    cxx = args.prf == "cxx"
+    flags = 3 | (_native.HB_ENCODE_SINGLE_PASS if args.single_pass else 0) | (_native.HB_PRF_CXX if cxx else 0)
 
     def step():
         ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, b0, dptr, length, nblocks, tptr,
@@ -158,10 +162,15 @@ def main():
     # nb = 32 byte-0 AES-256 per try (197 LDS lookups each); the two-pass
     # encode replaces the first 4 of every block's first try by prefix-image
     # loads and builds that image (2^24 + 2^16 + 2^8 AES) once per step
-    aes = tries.value * 32
-    if not args.single_pass:
-        aes += (1 << 24) + (1 << 16) + (1 << 8) - 4 * nblocks
-    lookups = aes * (16 * 12 + 5)
+    if cxx:
+        # cxx prf: 2 full AES-256 per try (CFB-128 over 32 bytes), 16 * 14 lookups each
+        aes = tries.value * 2
+        lookups = aes * 16 * 14
+    else:
+        aes = tries.value * 32
+        if not args.single_pass:
+            aes += (1 << 24) + (1 << 16) + (1 << 8) - 4 * nblocks
+        lookups = aes * (16 * 12 + 5)
     lds_rate = lookups / (kernel_ms * 1e-3)
     lds_peak = NUM_CUS * CLOCK_GHZ * 1e9 * LDS_LOOKUPS_PER_CLK_CU
 
@@ -169,7 +178,7 @@ def main():
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
-            rec = json.load(open(prof)).get(args.config)
+            rec = json.load(open(prof)).get(args.config + ("_cxx" if cxx else ""))
             if rec and rec.get("file_bytes") == length:
                 traffic = rec["hbm_bytes_per_launch"]
         except (ValueError, KeyError):
@@ -197,6 +206,8 @@ def main():
             "prime_bits": 256,
             "prime": hex(p),
             "expected_tries_per_prf": round(2.0 ** 256 / p, 4),
+            "prf": "cxx Swizzle prf (cxx/prf.hxx:125-176, CFB-128 over SHA256(LE32 i)); parity unpinned"
+                   if cxx else "PySwizzle KeyedPRF (util.py:83-96, CFB-8 over SHA256(str(i))); bit-exact",
             "parallelism": "dp%d block-range shards, no collective" % world,
         },
         "roofline": {
@@ -206,7 +217,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": "hb_encode_kernel" if args.single_pass else
+            "kernel": "hb_cxx_encode_kernel" if cxx else "hb_encode_kernel" if args.single_pass else
                       "hb_prefix_kernel + hb_encode_first_kernel + hb_encode_retry_kernel",
             "kernel_ms": round(kernel_ms, 3),
             "algorithmic_bytes_per_launch": length,
@@ -223,7 +234,7 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C,
-                                            args.cpu_seconds, args.cpu_threads)
+                                            args.cpu_seconds, args.cpu_threads, cxx)
     if rank == 0 and args.host_path:
         line["host_path"] = host_path(ctx, L, dptr, length, S, pb, fk, ak, C)
 
@@ -298,7 +309,7 @@ def bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak
     ctx.check(L.hb_device_free(ctx.h, tptr))
 
 
-def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads):
+def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads, cxx=False):
     """Oracle (kind "port") on successive 256 MiB prefixes of the same file
     until `seconds` of CPU work, on `threads` host threads."""
     import numpy as np
@@ -315,7 +326,7 @@ def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads):
         ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value + off, n, 2))
         nb = n // C
         t = time.perf_counter()
-        rc = O.encode_raw(p, S, fk, ak, host.ctypes.data, n, off // C, nb, out.ctypes.data, threads)
+        rc = O.encode_raw(p, S, fk, ak, host.ctypes.data, n, off // C, nb, out.ctypes.data, threads, cxx)
         busy += time.perf_counter() - t
         if rc:
             raise RuntimeError("oracle error %d" % rc)
@@ -324,8 +335,10 @@ def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads):
     return {"value": round(done / GIB / busy, 4), "unit": "GiB/s", "cores": threads,
             "kind": "port",
             "sample": "%d MiB prefix of the same synthetic file (%d blocks), oracle/swizzle_oracle.c "
-                      "(OpenSSL AES-NI CFB8 + BIGNUM), %d pthreads, %.1f s" % (
-                          done >> 20, done // C, threads, busy)}
+                      "(%s), %d pthreads, %.1f s" % (
+                          done >> 20, done // C,
+                          "cxx prf: OpenSSL AES-NI CFB-128 + BIGNUM" if cxx else
+                          "OpenSSL AES-NI CFB8 + BIGNUM", threads, busy)}
 
 
 def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):

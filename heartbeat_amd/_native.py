@@ -18,6 +18,8 @@ LIB_PATH = os.environ.get("HB_LIB_PATH") or os.path.join(HERE, "libhbswizzle.so"
 HB_DATA_ON_DEVICE = 1
 HB_TAGS_ON_DEVICE = 2
 HB_ENCODE_SINGLE_PASS = 4
+HB_EUNSUPPORTED = -4
+HB_PRF_CXX = 8
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -49,6 +51,7 @@ SIGNATURES = [
     ("hb_device_malloc", _c.c_int, [_P, _c.c_uint64, _c.POINTER(_P)]),
     ("hb_device_free", _c.c_int, [_P, _P]),
     ("hb_memcpy", _c.c_int, [_P, _P, _P, _c.c_uint64, _c.c_int]),
+    ("hb_cxx_prf_eval", _c.c_int, [_P, _B, _c.c_size_t, _B, _c.c_size_t, _P, _c.c_size_t, _P]),
     ("hb_host_register", _c.c_int, [_P, _P, _c.c_uint64]),
     ("hb_host_unregister", _c.c_int, [_P, _P]),
     ("hb_fill_random", _c.c_int, [_P, _P, _c.c_uint64, _c.c_uint64]),

@@ -45,4 +45,4 @@ hipError_t hb_launch_fill(unsigned char *dst, u64 len, u64 seed, hipStream_t s) 
     return hipGetLastError();
 }
 
-template hipError_t hb_launch_prf<2>(const PrfArgs<2> &, int, int, hipStream_t);
+template hipError_t hb_launch_prf<2>(const PrfArgs<2> &, int, int, int, hipStream_t);

@@ -107,7 +107,15 @@ struct HbPool {
 // The PRF engine: runs KeyedPRF.eval for every job of the queue and calls
 // h.accept(job, value) once per job with the accepted value.  h.init(job, sr)
 // sets the CFB-8 shift register a job starts from (zero for a fresh eval).
-template <int NL, int NR, class H>
+// MODE 0: KeyedPRF (util.py:83-96); MODE 1: the cxx prf (prf.hxx:125-176,
+// hb_cxx_try), whose x is an unsigned int and which accepts after 81 tries.
+template <int MODE>
+__device__ __forceinline__ void hb_prf_digest(u64 x, u32 dig[8]) {
+    if (MODE == 1) hb_sha256_le32((u32)x, dig);
+    else hb_sha256_decimal(x, dig);
+}
+
+template <int NL, int NR, class H, int MODE = 0>
 __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParams<NL> &P,
                                           u64 njobs, unsigned long long *queue) {
     HbPool pool{0, 0, njobs, queue, false};
@@ -116,13 +124,16 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
     u32 dig[8], sr[4] = {0, 0, 0, 0}, out[NL];
     if (active) {
         h.init(job, sr);
-        hb_sha256_decimal(h.x_of(job), dig);
+        hb_prf_digest<MODE>(h.x_of(job), dig);
     }
     u32 tries = 0, job_tries = 0, failed = 0;
     while (__ballot(active)) {
-        const u32 ok = hb_prf_try<NL, NR>(L, P, sr, dig, out);
+        u32 ok;
+        if constexpr (MODE == 1) ok = hb_cxx_try<NL, NR>(L, P, sr, dig, out);
+        else ok = hb_prf_try<NL, NR>(L, P, sr, dig, out);
         tries += active ? 1u : 0u;
         job_tries += 1u;
+        if (MODE == 1 && job_tries >= HB_CXX_MAX_TRIES) ok = 1;   // `count++ < 80` (prf.hxx:142)
         const bool acc = active && ok;
         if (acc) h.accept(job, out);
         // Exit guarantee: a job still rejected after HB_MAX_TRIES tries
@@ -141,7 +152,7 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
                 job_tries = 0;
                 if (got) {
                     h.init(job, sr);   // fresh cipher per eval (util.py:88) or a resumed stream
-                    hb_sha256_decimal(h.x_of(job), dig);
+                    hb_prf_digest<MODE>(h.x_of(job), dig);
                 }
             }
         }
@@ -169,7 +180,7 @@ struct HbEncodeOcc { static constexpr int v = NL <= 8 ? HB_OCC8 : 1; };
 
 __device__ __forceinline__ void hb_zero_sr(u32 sr[4]) { sr[0] = sr[1] = sr[2] = sr[3] = 0; }
 
-template <int NL, int ALIGN>
+template <int NL, int ALIGN, int MODE = 0>
 struct EncodeHandler {
     const EncodeArgs<NL> &A;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.block_base + job; }
@@ -178,6 +189,12 @@ struct EncodeHandler {
 #if defined(HB_EXP_NO_MAC)
         hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, F);
 #else
+        if (MODE == 1 && job * A.C >= A.len) {
+            // cxx: no sector read -> sigma = f(chunk_id) without `%= p`
+            // (shacham_waters_private.cxx:681-690; differs only if F >= p)
+            hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, F);
+            return;
+        }
         u32 tag[NL];
         hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
         hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, tag);
@@ -192,6 +209,18 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_ke
     const LaneTab L = hb_lane_tab(lds);
     EncodeHandler<NL, ALIGN> h{A};
     hb_engine<NL, NR>(h, L, A.prf, A.nblocks, A.queue);
+}
+
+// The cxx Swizzle encode (shacham_waters_private.cxx:638-702): the same
+// engine and MAC with the cxx prf (CFB-128: nb/16 full AES per try instead of
+// nb byte-0 AES).
+template <int NL, int NR, int ALIGN>
+__global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_cxx_encode_kernel(EncodeArgs<NL> A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L = hb_lane_tab(lds);
+    EncodeHandler<NL, ALIGN, 1> h{A};
+    hb_engine<NL, NR, EncodeHandler<NL, ALIGN, 1>, 1>(h, L, A.prf, A.nblocks, A.queue);
 }
 
 // ------------------------------------------------------------------ two-pass encode
@@ -343,13 +372,13 @@ struct PrfHandler {
     }
 };
 
-template <int NL, int NR>
+template <int NL, int NR, int MODE>
 __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prf_kernel(PrfArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     PrfHandler<NL> h{A};
-    hb_engine<NL, NR>(h, L, A.prf, A.n, A.queue);
+    hb_engine<NL, NR, PrfHandler<NL>, MODE>(h, L, A.prf, A.n, A.queue);
 }
 
 // ------------------------------------------------------------------ Montgomery
@@ -452,7 +481,8 @@ __global__ __launch_bounds__(256) void hb_sum_kernel(SumArgs<NL> A) {
 // ------------------------------------------------------------------ launchers
 // Plain C++ entry points for hb_runtime.cpp (explicit instantiation per
 // limb count NL, AES rounds NR and sector alignment class).
-// pass: 0 = single-pass engine, 1 = first tries (prefix image), 2 = retry list
+// pass: 0 = single-pass engine, 1 = first tries (prefix image), 2 = retry list,
+// 3 = cxx prf encode
 template <int NL>
 hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
@@ -462,6 +492,7 @@ hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass
 #define HB_ENC_AL(K) do { if (align == 16) HB_ENC_NR(K, 16); else HB_ENC_NR(K, 1); } while (0)
     if (pass == 1) HB_ENC_AL(hb_encode_first_kernel);
     else if (pass == 2) HB_ENC_AL(hb_encode_retry_kernel);
+    else if (pass == 3) HB_ENC_AL(hb_cxx_encode_kernel);
     else HB_ENC_AL(hb_encode_kernel);
 #undef HB_ENC_AL
 #undef HB_ENC_NR
@@ -470,12 +501,23 @@ hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass
 }
 
 
+// mode 0: KeyedPRF, 1: cxx prf
 template <int NL>
-hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int grid, hipStream_t s) {
+hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int mode, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
-    if (nr == 14) hipLaunchKernelGGL((hb_prf_kernel<NL, 14>), g, b, 0, s, A);
-    else if (nr == 12) hipLaunchKernelGGL((hb_prf_kernel<NL, 12>), g, b, 0, s, A);
-    else hipLaunchKernelGGL((hb_prf_kernel<NL, 10>), g, b, 0, s, A);
+#define HB_PRF_NR(M)                                                               \
+    do {                                                                           \
+        if (nr == 14) hipLaunchKernelGGL((hb_prf_kernel<NL, 14, M>), g, b, 0, s, A); \
+        else if (nr == 12) hipLaunchKernelGGL((hb_prf_kernel<NL, 12, M>), g, b, 0, s, A); \
+        else hipLaunchKernelGGL((hb_prf_kernel<NL, 10, M>), g, b, 0, s, A);       \
+    } while (0)
+    if (mode == 1) {
+        if constexpr (NL >= 4) HB_PRF_NR(1);   // cxx limits are >= 16 bytes
+        else return hipErrorInvalidValue;
+    } else {
+        HB_PRF_NR(0);
+    }
+#undef HB_PRF_NR
     return hipGetLastError();
 }
 
@@ -502,7 +544,7 @@ hipError_t hb_launch_sum(const SumArgs<NL> &A, int ncols, hipStream_t s) {
 
 #define HB_INST(NL)                                                                              \
     template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t); \
-    template hipError_t hb_launch_prf<NL>(const PrfArgs<NL> &, int, int, hipStream_t);           \
+    template hipError_t hb_launch_prf<NL>(const PrfArgs<NL> &, int, int, int, hipStream_t);      \
     template hipError_t hb_launch_mont<NL>(const MontArgs<NL> &, hipStream_t);                   \
     template hipError_t hb_launch_wsum<NL>(const WsumArgs<NL> &, int, int, hipStream_t);         \
     template hipError_t hb_launch_sum<NL>(const SumArgs<NL> &, int, hipStream_t);

@@ -151,27 +151,9 @@ HB_HD void hb_aes_byte0_n(const LaneTab &L, const u32 *rk, const u32 s[N][4], u3
 // ------------------------------------------------------------------ SHA-256
 HB_HD u32 hb_rotr(u32 x, u32 n) { return hb_alignbit(x, x, n); }
 
-// SHA-256 of ASCII decimal(x) (str(x).encode(), util.py:91); one compression
-// since len <= 20 < 56.  Digest as 8 big-endian words.
-HB_HD void hb_sha256_decimal(u64 x, u32 H[8]) {
-    // Build the message right-to-left: shifting a 24-byte big-endian register
-    // right by one byte per digit and inserting the digit at the top leaves
-    // the decimal string left-aligned with the 0x80 pad byte right behind it.
-    u32 R0 = 0x80000000u, R1 = 0, R2 = 0, R3 = 0, R4 = 0, R5 = 0;
-    u32 n = 0;
-    do {
-        u64 q = x / 10u;
-        u32 dgt = (u32)(x - q * 10u);
-        x = q;
-        R5 = hb_alignbit(R4, R5, 8);
-        R4 = hb_alignbit(R3, R4, 8);
-        R3 = hb_alignbit(R2, R3, 8);
-        R2 = hb_alignbit(R1, R2, 8);
-        R1 = hb_alignbit(R0, R1, 8);
-        R0 = (R0 >> 8) | ((0x30u + dgt) << 24);
-        ++n;
-    } while (x != 0);
-    u32 W[16] = {R0, R1, R2, R3, R4, R5, 0, 0, 0, 0, 0, 0, 0, 0, 0, n * 8u};
+// One SHA-256 compression from the initial state over the padded message
+// block W (16 big-endian words, clobbered).  Digest as 8 big-endian words.
+HB_HD void hb_sha256_block(u32 W[16], u32 H[8]) {
     const u32 K[64] = {
         0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
         0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
@@ -208,6 +190,37 @@ HB_HD void hb_sha256_decimal(u64 x, u32 H[8]) {
     }
     H[0] = a + 0x6a09e667u; H[1] = b + 0xbb67ae85u; H[2] = c + 0x3c6ef372u; H[3] = d + 0xa54ff53au;
     H[4] = e + 0x510e527fu; H[5] = f + 0x9b05688cu; H[6] = g + 0x1f83d9abu; H[7] = h + 0x5be0cd19u;
+}
+
+// SHA-256 of ASCII decimal(x) (str(x).encode(), util.py:91); one compression
+// since len <= 20 < 56.  Digest as 8 big-endian words.
+HB_HD void hb_sha256_decimal(u64 x, u32 H[8]) {
+    // Build the message right-to-left: shifting a 24-byte big-endian register
+    // right by one byte per digit and inserting the digit at the top leaves
+    // the decimal string left-aligned with the 0x80 pad byte right behind it.
+    u32 R0 = 0x80000000u, R1 = 0, R2 = 0, R3 = 0, R4 = 0, R5 = 0;
+    u32 n = 0;
+    do {
+        u64 q = x / 10u;
+        u32 dgt = (u32)(x - q * 10u);
+        x = q;
+        R5 = hb_alignbit(R4, R5, 8);
+        R4 = hb_alignbit(R3, R4, 8);
+        R3 = hb_alignbit(R2, R3, 8);
+        R2 = hb_alignbit(R1, R2, 8);
+        R1 = hb_alignbit(R0, R1, 8);
+        R0 = (R0 >> 8) | ((0x30u + dgt) << 24);
+        ++n;
+    } while (x != 0);
+    u32 W[16] = {R0, R1, R2, R3, R4, R5, 0, 0, 0, 0, 0, 0, 0, 0, 0, n * 8u};
+    hb_sha256_block(W, H);
+}
+
+// SHA-256 of the 4 raw bytes of a 32-bit unsigned int in x86 (little-endian)
+// order: the cxx prf's message (cxx/prf.hxx:174, (unsigned char*)&i).
+HB_HD void hb_sha256_le32(u32 x, u32 H[8]) {
+    u32 W[16] = {hb_bswap(x), 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 32u};
+    hb_sha256_block(W, H);
 }
 
 // ------------------------------------------------------------------ PRF try
@@ -286,6 +299,76 @@ template <int NL, int NR>
 HB_HD u32 hb_prf_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const u32 dig[8],
                      u32 out[NL]) {
     return hb_prf_try_from<NL, NR, 0>(L, P, sr, dig, out);
+}
+
+// ------------------------------------------------------------------ cxx prf
+// The cxx Swizzle extension's PRF F' (cxx/prf.hxx:125-176), a different
+// function from KeyedPRF: one Crypto++ CFB_Mode<AES> (full 16-byte feedback,
+// IV = 0^16) resynchronised once per evaluate (:132); every try
+// (rand_buf, :170-176) encrypts buf = SHA256(LE32(i)) zero-padded (or
+// truncated) to limit_sz = ByteCount(limit) bytes, the stream continuing
+// across tries; a = BE(buf) with the top byte masked to the bit length of the
+// limit's top byte (set_limit :97-116, clz.h:36-48: 32-bit clz of a positive
+// int, so the mask is 2^bitlen(b) - 1 = KeyedPRF's topmask); accepted when
+// a < limit, or unconditionally after 81 tries (`count++ < 80`, :135-142).
+#define HB_CXX_MAX_TRIES 81u
+
+// All 16 output bytes of AES_k(w) in place (little-endian column words).  The
+// last round's S[x] is byte k of T_{(k+2)&3}[x]: T0 = (2S, S, S, 3S),
+// T1 = (3S, 2S, S, S), T2 = (S, 3S, 2S, S), T3 = (S, S, 3S, 2S).
+template <int NR>
+HB_HD void hb_aes_full(const LaneTab &L, const u32 *rk, u32 &w0, u32 &w1, u32 &w2, u32 &w3) {
+    w0 ^= rk[0]; w1 ^= rk[1]; w2 ^= rk[2]; w3 ^= rk[3];
+    HB_UNROLL
+    for (int r = 1; r <= NR - 1; ++r) hb_aes_round(L, rk + 4 * r, w0, w1, w2, w3);
+    const u32 *k = rk + 4 * NR;
+    const u32 o0 = (hb_t<0, 2>(L, w0) & 0xffu) | (hb_t<1, 3>(L, w1) & 0xff00u) |
+                   (hb_t<2, 0>(L, w2) & 0xff0000u) | (hb_t<3, 1>(L, w3) & 0xff000000u);
+    const u32 o1 = (hb_t<0, 2>(L, w1) & 0xffu) | (hb_t<1, 3>(L, w2) & 0xff00u) |
+                   (hb_t<2, 0>(L, w3) & 0xff0000u) | (hb_t<3, 1>(L, w0) & 0xff000000u);
+    const u32 o2 = (hb_t<0, 2>(L, w2) & 0xffu) | (hb_t<1, 3>(L, w3) & 0xff00u) |
+                   (hb_t<2, 0>(L, w0) & 0xff0000u) | (hb_t<3, 1>(L, w1) & 0xff000000u);
+    const u32 o3 = (hb_t<0, 2>(L, w3) & 0xffu) | (hb_t<1, 3>(L, w0) & 0xff00u) |
+                   (hb_t<2, 0>(L, w1) & 0xff0000u) | (hb_t<3, 1>(L, w2) & 0xff000000u);
+    w0 = o0 ^ k[0]; w1 = o1 ^ k[1]; w2 = o2 ^ k[2]; w3 = o3 ^ k[3];
+}
+
+// One try of F': nb / 16 CFB-128 blocks (P.nb = limit_sz, a multiple of 16,
+// <= 4 NL -- checked on the host) continuing from the feedback register sr
+// (the previous ciphertext block, little-endian words; 0 = the IV).
+// dig: SHA256(LE32(i)) as big-endian words; plaintext = dig then zeros.
+// out = masked BE(ciphertext) in NL little-endian limbs; returns out < limit.
+template <int NL, int NR>
+HB_HD u32 hb_cxx_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const u32 dig[8],
+                     u32 out[NL]) {
+    static_assert(NL >= 4, "cxx prf limits are at least 16 bytes");
+    HB_UNROLL
+    for (int t = 0; t < NL; ++t) out[t] = 0;
+    u32 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
+    const u32 nblk = P.nb >> 4;
+    HB_NOUNROLL
+    for (u32 k = 0; k < nblk; ++k) {
+        hb_aes_full<NR>(L, P.rk, r0, r1, r2, r3);
+        // plaintext words of block k (bytes 16k..16k+15 of dig || 0...)
+        const u32 p0 = k == 0 ? dig[0] : k == 1 ? dig[4] : 0u, p1 = k == 0 ? dig[1] : k == 1 ? dig[5] : 0u;
+        const u32 p2 = k == 0 ? dig[2] : k == 1 ? dig[6] : 0u, p3 = k == 0 ? dig[3] : k == 1 ? dig[7] : 0u;
+        r0 ^= hb_bswap(p0); r1 ^= hb_bswap(p1); r2 ^= hb_bswap(p2); r3 ^= hb_bswap(p3);
+        // ciphertext block k = the next feedback register; append it to out
+        // (big-endian words, the first block ends up most significant)
+        u32 b0 = hb_bswap(r0);
+        if (k == 0) b0 &= (P.topmask << 24) | 0xffffffu;
+        HB_UNROLL
+        for (int t = NL - 1; t >= 4; --t) out[t] = out[t - 4];
+        out[3] = b0; out[2] = hb_bswap(r1); out[1] = hb_bswap(r2); out[0] = hb_bswap(r3);
+    }
+    sr[0] = r0; sr[1] = r1; sr[2] = r2; sr[3] = r3;
+    u32 borrow = 0;
+    HB_UNROLL
+    for (int t = 0; t < NL; ++t) {
+        u64 d = (u64)out[t] - (u64)P.R[t] - (u64)borrow;
+        borrow = (u32)(d >> 63);
+    }
+    return borrow;
 }
 
 // ------------------------------------------------------------------ CFB prefix

@@ -25,7 +25,7 @@ using namespace hbhost;
 // launchers (hb_kernels.hip)
 template <int NL> hipError_t hb_launch_encode(const EncodeArgs<NL> &, int, int, int, int, hipStream_t);
 hipError_t hb_launch_prefix(const PrefixArgs &, int, int, hipStream_t);
-template <int NL> hipError_t hb_launch_prf(const PrfArgs<NL> &, int, int, hipStream_t);
+template <int NL> hipError_t hb_launch_prf(const PrfArgs<NL> &, int, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_mont(const MontArgs<NL> &, hipStream_t);
 template <int NL> hipError_t hb_launch_wsum(const WsumArgs<NL> &, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_sum(const SumArgs<NL> &, int, hipStream_t);
@@ -137,7 +137,7 @@ int check_key(hb_ctx *c, size_t key_len) {
 // results as NL-limb little-endian values in out (device).
 template <int NL>
 int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be, size_t range_len,
-            const u64 *xs_dev, u64 x0, u64 n, u32 *out_dev, int queue_slot) {
+            const u64 *xs_dev, u64 x0, u64 n, u32 *out_dev, int queue_slot, int mode = 0) {
     PrfArgs<NL> A;
     int nr = 0;
     if (!make_prf<NL>(key, key_len, range_be, range_len, A.prf, nr))
@@ -150,7 +150,7 @@ int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_
     A.queue = c->queue + HB_QSLOT * queue_slot;
     if (n == 0) return 0;
     HB_CHECK(hipMemsetAsync(A.queue, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
-    HB_CHECK(hb_launch_prf<NL>(A, nr, engine_grid(c, n), c->stream), "hb_prf_kernel launch");
+    HB_CHECK(hb_launch_prf<NL>(A, nr, mode, engine_grid(c, n), c->stream), "hb_prf_kernel launch");
     return 0;
 }
 
@@ -234,7 +234,10 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // alpha_j R mod p, j < S  (alpha = KeyedPRF(alpha_key, p), PySwizzle.py:291,302)
     HB_CHECK(c->alpha_raw.ensure((size_t)S * NL * 4), "hipMalloc");
     HB_CHECK(c->alpha_mont.ensure((size_t)S * NL * 4), "hipMalloc");
-    int rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1);
+    const bool cxx = flags & HB_PRF_CXX;
+    if (cxx && (pi.tw % 16 != 0 || pi.tw > 4u * NL))
+        return fail(c, HB_EUNSUPPORTED, "cxx prf mode needs ByteCount(p) to be a multiple of 16");
+    int rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, cxx ? 1 : 0);
     if (rc) return rc;
     rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S);
     if (rc) return rc;
@@ -265,7 +268,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     u64 cb = C ? (256ull << 20) / C : 1;
     if (cb < 1) cb = 1;
     const u64 launch_blocks = data_dev ? nblocks : (nblocks < cb ? nblocks : cb);
-    const bool two_pass = A.prf.nb >= 4 && !(flags & HB_ENCODE_SINGLE_PASS);
+    const bool two_pass = !cxx && A.prf.nb >= 4 && !(flags & HB_ENCODE_SINGLE_PASS);
     if (two_pass) {
         HB_CHECK(c->pfx.ensure(HB_PFX_BYTES), "hipMalloc(prefix)");
         A.retry_cap = retry_capacity(p_be, p_len, launch_blocks);
@@ -304,7 +307,8 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(hipMemsetAsync(q0, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
         if (!two_pass) {
             A.queue = q0;
-            HB_CHECK(hb_launch_encode<NL>(A, nr, align, 0, engine_grid(c, nb), c->stream), "hb_encode_kernel launch");
+            HB_CHECK(hb_launch_encode<NL>(A, nr, align, cxx ? 3 : 0, engine_grid(c, nb), c->stream),
+                     "hb_encode_kernel launch");
             c->last_launches++;
             return 0;
         }
@@ -697,6 +701,39 @@ int hb_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *ra
     if (int rc2 = check_prf_slots(c)) return rc2;
     const size_t nb = (size_t)(bits + 7) / 8;
     for (size_t i = 0; i < n; ++i) to_be(&h[i * nl], (size_t)nl, out + i * nb, nb);
+    return 0;
+}
+
+int hb_cxx_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *limit_be,
+                    size_t limit_len, const uint32_t *xs, size_t n, uint8_t *out) {
+    if (!c) return HB_EINVAL;
+    if (int rc = check_key(c, key_len)) return rc;
+    const int bits = bitlen_be(limit_be, limit_len);
+    if (bits == 0) return fail(c, HB_EINVAL, "PRF limit must be positive");
+    const int nl = nl_for_bits(bits);
+    const size_t nb = (size_t)(bits + 7) / 8;
+    if (!nl) return fail(c, HB_EUNSUPPORTED, "PRF limits above 1024 bits are not supported by this build");
+    if (nb % 16) return fail(c, HB_EUNSUPPORTED, "cxx prf mode needs ByteCount(limit) to be a multiple of 16");
+    if (n == 0) return 0;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    std::vector<u64> x64(n);
+    for (size_t i = 0; i < n; ++i) x64[i] = xs[i];
+    const int nlv = nl < 8 ? 8 : nl;
+    HB_CHECK(c->xs.ensure(n * 8), "hipMalloc");
+    HB_CHECK(c->vals.ensure(n * (size_t)nlv * 4), "hipMalloc");
+    HB_CHECK(hipMemcpyAsync(c->xs.p, x64.data(), n * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+    int rc = 0;
+    switch (nlv) {
+    case 8: rc = run_prf<8>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, 1); break;
+    case 16: rc = run_prf<16>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, 1); break;
+    default: rc = run_prf<32>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, 1); break;
+    }
+    if (rc) return rc;
+    std::vector<u32> h(n * (size_t)nlv);
+    HB_CHECK(hipMemcpyAsync(h.data(), c->vals.p, h.size() * 4, hipMemcpyDeviceToHost, c->stream), "D2H");
+    HB_CHECK(hipStreamSynchronize(c->stream), "hb_prf_kernel");
+    if (int rc2 = check_prf_slots(c)) return rc2;
+    for (size_t i = 0; i < n; ++i) to_be(&h[i * nlv], (size_t)nlv, out + i * nb, nb);
     return 0;
 }
 

@@ -43,6 +43,12 @@ extern "C" {
 #define HB_ENCODE_SINGLE_PASS 4u  /* hb_encode: one-pass engine instead of the
                                      prefix-image first pass + retry pass (same
                                      tags; for A/B tests and measurements) */
+#define HB_PRF_CXX 8u  /* hb_encode: the cxx Swizzle extension's PRF (cxx/prf.hxx:125-176:
+                          CFB-128 over SHA256(LE32 i), <= 81 tries) and encode loop
+                          (cxx/shacham_waters_private.cxx:638-702) instead of PySwizzle's
+                          KeyedPRF; needs ByteCount(p) % 16 == 0 (the cxx API's 1024-bit
+                          primes, 256-bit primes).  Tags differ from PySwizzle's.
+                          Parity unpinned (Crypto++ absent). */
 
 /* error codes */
 #define HB_OK 0
@@ -95,6 +101,13 @@ int hb_encode(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
               uint64_t block_base, const uint8_t *data, uint64_t len,
               uint64_t nblocks, uint8_t *tags, uint32_t flags,
               uint64_t *tries_out);
+
+/* The cxx prf, prf::evaluate(i) (cxx/prf.hxx:125-145), for n unsigned-int
+ * inputs, keyed by key and bounded by limit (ByteCount(limit) % 16 == 0):
+ * out receives n values of ByteCount(limit) big-endian bytes each. */
+int hb_cxx_prf_eval(hb_ctx *ctx, const uint8_t *key, size_t key_len,
+                    const uint8_t *limit_be, size_t limit_len,
+                    const uint32_t *xs, size_t n, uint8_t *out);
 
 /* len/C + 1: the number of tags PySwizzle.encode produces for a file. */
 uint64_t hb_block_count(const uint8_t *p_be, size_t p_len, uint32_t sectors,

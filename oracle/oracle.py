@@ -31,6 +31,9 @@ def lib():
         L.hbo_encode.argtypes = [c.c_char_p, c.c_size_t, c.c_uint32, c.c_char_p, c.c_char_p,
                                  c.c_size_t, c.c_uint64, c.c_void_p, c.c_uint64, c.c_uint64,
                                  c.c_void_p, c.c_int]
+        L.hbo_cxx_prf_eval.argtypes = [c.c_char_p, c.c_size_t, c.c_char_p, c.c_size_t,
+                                       c.c_uint32, c.c_char_p, c.c_size_t]
+        L.hbo_cxx_encode.argtypes = L.hbo_encode.argtypes
         L.hbo_prove.argtypes = [c.c_char_p, c.c_size_t, c.c_uint32, c.c_char_p, c.c_size_t,
                                 c.c_uint64, c.c_char_p, c.c_size_t, c.c_uint64, c.c_char_p,
                                 c.c_int, c.c_void_p, c.c_uint64, c.c_char_p, c.c_char_p]
@@ -80,7 +83,8 @@ def width_of(p):
     return (int(p).bit_length() + 7) // 8
 
 
-def encode(p, sectors, f_key, alpha_key, data, block_base=0, nblocks=None, nthreads=1):
+def encode(p, sectors, f_key, alpha_key, data, block_base=0, nblocks=None, nthreads=1,
+           _fn="hbo_encode"):
     """Tags (list of ints) of PySwizzle.encode for the given keys."""
     p = int(p)
     ss = p.bit_length() // 8
@@ -91,8 +95,8 @@ def encode(p, sectors, f_key, alpha_key, data, block_base=0, nblocks=None, nthre
     out = ctypes.create_string_buffer(w * max(nblocks, 1))
     addr, n = _addr(data)
     pb = _be(p)
-    rc = lib().hbo_encode(pb, len(pb), sectors, bytes(f_key), bytes(alpha_key), len(f_key),
-                          block_base, addr, n, nblocks, out, nthreads)
+    rc = getattr(lib(), _fn)(pb, len(pb), sectors, bytes(f_key), bytes(alpha_key), len(f_key),
+                             block_base, addr, n, nblocks, out, nthreads)
     if rc:
         raise ValueError("oracle encode error %d" % rc)
     raw = out.raw
@@ -100,11 +104,27 @@ def encode(p, sectors, f_key, alpha_key, data, block_base=0, nblocks=None, nthre
 
 
 def encode_raw(p, sectors, f_key, alpha_key, data_addr, data_len, block_base, nblocks,
-               out_addr, nthreads):
+               out_addr, nthreads, cxx=False):
     """Zero-copy variant for the CPU baseline: raw addresses in and out."""
     pb = _be(p)
-    return lib().hbo_encode(pb, len(pb), sectors, bytes(f_key), bytes(alpha_key), len(f_key),
+    return (lib().hbo_cxx_encode if cxx else lib().hbo_encode)(pb, len(pb), sectors, bytes(f_key), bytes(alpha_key), len(f_key),
                             block_base, data_addr, data_len, nblocks, out_addr, nthreads)
+
+
+def cxx_prf_eval(key, limit, i):
+    """cxx prf::evaluate(i) (cxx/prf.hxx:125-145) -> (value, tries).  Parity unpinned."""
+    lb = _be(limit)
+    nb = (int(limit).bit_length() + 7) // 8
+    out = ctypes.create_string_buffer(nb)
+    tries = lib().hbo_cxx_prf_eval(bytes(key), len(key), lb, len(lb), int(i) & 0xffffffff, out, nb)
+    if tries <= 0:
+        raise ValueError("oracle cxx prf error %d" % tries)
+    return int.from_bytes(out.raw, "big"), tries
+
+
+def cxx_encode(p, sectors, f_key, alpha_key, data, block_base=0, nblocks=None, nthreads=1):
+    """cxx shacham_waters_private::encode tags (list of ints).  Parity unpinned."""
+    return encode(p, sectors, f_key, alpha_key, data, block_base, nblocks, nthreads, _fn="hbo_cxx_encode")
 
 
 def prove(p, sectors, chal_key, chunks, v_max, tags, data):

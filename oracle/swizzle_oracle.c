@@ -22,6 +22,16 @@
  *                  read (:298-306).  Always floor(L/C)+1 tags.
  *   hbo_prove      PySwizzle.py:333-370
  *   hbo_verify     PySwizzle.py:372-395
+ *   hbo_cxx_prf_eval / hbo_cxx_encode (mode 1): the cxx Swizzle extension's
+ *                  PRF and encode loop, cxx/prf.hxx:97-176 (+ cxx/clz.h:36-48)
+ *                  and cxx/shacham_waters_private.cxx:638-702: CFB-128 (full
+ *                  block feedback, IV 0, resynchronised per evaluate) over
+ *                  SHA256(LE32(i)) padded to ByteCount(limit), stream continuing
+ *                  across tries, at most 81 tries; sigma %= p only after a
+ *                  sector was read.  PARITY UNPINNED: Crypto++ is absent here,
+ *                  so no reference output pins it; OpenSSL's
+ *                  CFB-128 is the same primitive as CFB_Mode<AES> with full-block
+ *                  feedback (SP 800-38A vectors).
  *
  * Arithmetic: OpenSSL BIGNUM (exact).  AES/SHA: OpenSSL EVP (AES-NI when the
  * host has it).  Threads: hbo_encode splits the block range into contiguous
@@ -40,6 +50,7 @@
 
 typedef struct {
     EVP_CIPHER_CTX *ctx;
+    int mode;               /* 0 KeyedPRF (util.py), 1 cxx prf (prf.hxx) */
     BIGNUM *range;
     int nb;                 /* ceil(bitlen(range)/8)          util.py:92 */
     unsigned char topmask;  /* mask on the most significant byte, util.py:81 */
@@ -54,10 +65,37 @@ static const EVP_CIPHER *cfb8_for(size_t keylen) {
     }
 }
 
+static const EVP_CIPHER *cfb128_for(size_t keylen) {
+    switch (keylen) {
+    case 16: return EVP_aes_128_cfb128();
+    case 24: return EVP_aes_192_cfb128();
+    case 32: return EVP_aes_256_cfb128();
+    default: return NULL;
+    }
+}
+
+/* cxx/clz.h:36-48 (the build never defines HAVE_GNU_CLZ): leading zeros of a
+ * positive int in 32 bits */
+static unsigned cxx_clz(int x) {
+    unsigned n = 0;
+    if (x == 0) return 32;
+    while (!(x & (int)0x80000000u)) { n++; x = (int)((unsigned)x << 1); }
+    return n;
+}
+
+static int prf_init_mode(prf_t *f, const unsigned char *key, size_t keylen,
+                         const unsigned char *range_be, size_t range_len, int mode);
+
 static int prf_init(prf_t *f, const unsigned char *key, size_t keylen,
                     const unsigned char *range_be, size_t range_len) {
+    return prf_init_mode(f, key, keylen, range_be, range_len, 0);
+}
+
+static int prf_init_mode(prf_t *f, const unsigned char *key, size_t keylen,
+                         const unsigned char *range_be, size_t range_len, int mode) {
     static const unsigned char zero_iv[16] = {0};
-    const EVP_CIPHER *c = cfb8_for(keylen);
+    const EVP_CIPHER *c = mode ? cfb128_for(keylen) : cfb8_for(keylen);
+    f->mode = mode;
     int bits;
     if (!c) return -1;
     f->range = BN_bin2bn(range_be, (int)range_len, NULL);
@@ -65,7 +103,13 @@ static int prf_init(prf_t *f, const unsigned char *key, size_t keylen,
     if (bits == 0) { BN_free(f->range); return -2; }   /* range 0: reference never terminates */
     f->nb = (bits + 7) / 8;
     if (f->nb > HBO_MAX_NB) { BN_free(f->range); return -3; }
-    {
+    if (mode) {   /* set_limit, prf.hxx:97-116: ByteCount, mask from clz of the top byte */
+        unsigned char top = range_be[range_len - (size_t)f->nb];
+        unsigned char m = 0;
+        int i;
+        for (i = 0; i < (int)(32 - cxx_clz(top)); i++) m |= (unsigned char)(1u << i);
+        f->topmask = m;
+    } else {
         int topbits = bits - 8 * (f->nb - 1);
         f->topmask = (unsigned char)((1u << topbits) - 1u);
     }
@@ -100,7 +144,44 @@ static int prf_eval(prf_t *f, uint64_t x, BIGNUM *out) {
     }
 }
 
+/* prf::evaluate(i) (prf.hxx:125-145) -> out; returns number of tries. */
+static int cxx_prf_eval(prf_t *f, uint32_t i, BIGNUM *out) {
+    static const unsigned char zero_iv[16] = {0};
+    unsigned char digest[32], buf[HBO_MAX_NB], ct[HBO_MAX_NB], le[4];
+    int len, tries = 0;
+    unsigned count = 0;
+    le[0] = (unsigned char)i; le[1] = (unsigned char)(i >> 8);
+    le[2] = (unsigned char)(i >> 16); le[3] = (unsigned char)(i >> 24);
+    EVP_EncryptInit_ex(f->ctx, NULL, NULL, NULL, zero_iv);          /* Resynchronize */
+    for (;;) {
+        tries++;
+        /* rand_buf (:170-176): memset limit_sz, digest into the buffer */
+        SHA256(le, 4, digest);
+        memset(buf, 0, (size_t)f->nb);
+        memcpy(buf, digest, f->nb < 32 ? (size_t)f->nb : 32u);
+        EVP_EncryptUpdate(f->ctx, ct, &len, buf, f->nb);
+        ct[0] &= f->topmask;                                            /* SetByte(limit_sz-1, ..) */
+        BN_bin2bn(ct, f->nb, out);
+        if (!(BN_cmp(out, f->range) >= 0 && count++ < 80)) return tries;
+    }
+}
+
 /* ------------------------------------------------------------------ API */
+
+int hbo_cxx_prf_eval(const unsigned char *key, size_t keylen,
+                     const unsigned char *range_be, size_t range_len,
+                     uint32_t x, unsigned char *out_be, size_t out_len) {
+    prf_t f;
+    BIGNUM *v;
+    int tries, rc = prf_init_mode(&f, key, keylen, range_be, range_len, 1);
+    if (rc) return rc;
+    v = BN_new();
+    tries = cxx_prf_eval(&f, x, v);
+    BN_bn2binpad(v, out_be, (int)out_len);
+    BN_free(v);
+    prf_free(&f);
+    return tries;
+}
 
 int hbo_prf_eval(const unsigned char *key, size_t keylen,
                  const unsigned char *range_be, size_t range_len,
@@ -138,6 +219,7 @@ typedef struct {
     uint64_t b0, b1;            /* block slice [b0,b1) relative to data */
     unsigned char *tags; int width;
     BIGNUM **alpha;             /* shared, read-only */
+    int mode;
     int rc;
 } enc_job_t;
 
@@ -148,20 +230,24 @@ static void *encode_worker(void *arg) {
     BIGNUM *p = BN_bin2bn(J->p_be, (int)J->p_len, NULL);
     BIGNUM *sigma = BN_new(), *m = BN_new(), *t = BN_new();
     uint64_t ss = (uint64_t)(BN_num_bits(p) / 8), C = ss * J->sectors, i;
-    J->rc = prf_init(&f, J->f_key, J->keylen, J->p_be, J->p_len);
+    J->rc = prf_init_mode(&f, J->f_key, J->keylen, J->p_be, J->p_len, J->mode);
     if (J->rc) goto out;
     for (i = J->b0; i < J->b1; i++) {
         uint32_t j;
-        prf_eval(&f, J->block_base + i, sigma);                 /* sigma = f.eval(chunk_id) */
+        if (J->mode)   /* s.f(chunk_id), unsigned int chunk_id (shacham_waters_private.cxx:672) */
+            cxx_prf_eval(&f, (uint32_t)(J->block_base + i), sigma);
+        else
+            prf_eval(&f, J->block_base + i, sigma);             /* sigma = f.eval(chunk_id) */
         for (j = 0; j < J->sectors; j++) {
             uint64_t r = read_sector(J->data, J->len, i * C + j * ss, ss, m);
             if (r > 0) {
                 BN_mul(t, J->alpha[j], m, bctx);
                 BN_add(sigma, sigma, t);
+                if (J->mode) BN_mod(sigma, sigma, p, bctx);      /* sigma %= _p (:685) */
             }
             if (r != ss) break;
         }
-        BN_mod(sigma, sigma, p, bctx);
+        if (!J->mode) BN_mod(sigma, sigma, p, bctx);
         BN_bn2binpad(sigma, J->tags + (size_t)(i * (uint64_t)J->width), J->width);
     }
     prf_free(&f);
@@ -175,10 +261,33 @@ out:
  * call starts at data[k*C]; bytes at or past `len` are end of file).  The
  * whole-file PySwizzle encode is block_base = 0, nblocks = len/C + 1.
  * Tags are written big-endian, `width` = ceil(bitlen(p)/8) bytes each. */
+static int encode_mode(const unsigned char *p_be, size_t p_len, uint32_t sectors,
+                       const unsigned char *f_key, const unsigned char *a_key, size_t keylen,
+                       uint64_t block_base, const unsigned char *data, uint64_t len,
+                       uint64_t nblocks, unsigned char *tags_out, int nthreads, int mode);
+
 int hbo_encode(const unsigned char *p_be, size_t p_len, uint32_t sectors,
                const unsigned char *f_key, const unsigned char *a_key, size_t keylen,
                uint64_t block_base, const unsigned char *data, uint64_t len,
                uint64_t nblocks, unsigned char *tags_out, int nthreads) {
+    return encode_mode(p_be, p_len, sectors, f_key, a_key, keylen, block_base, data, len, nblocks,
+                       tags_out, nthreads, 0);
+}
+
+/* cxx shacham_waters_private::encode (shacham_waters_private.cxx:638-702)
+ * with the cxx prf; same block/sector layout and tag count as hbo_encode. */
+int hbo_cxx_encode(const unsigned char *p_be, size_t p_len, uint32_t sectors,
+                   const unsigned char *f_key, const unsigned char *a_key, size_t keylen,
+                   uint64_t block_base, const unsigned char *data, uint64_t len,
+                   uint64_t nblocks, unsigned char *tags_out, int nthreads) {
+    return encode_mode(p_be, p_len, sectors, f_key, a_key, keylen, block_base, data, len, nblocks,
+                       tags_out, nthreads, 1);
+}
+
+static int encode_mode(const unsigned char *p_be, size_t p_len, uint32_t sectors,
+                       const unsigned char *f_key, const unsigned char *a_key, size_t keylen,
+                       uint64_t block_base, const unsigned char *data, uint64_t len,
+                       uint64_t nblocks, unsigned char *tags_out, int nthreads, int mode) {
     BIGNUM *p = BN_bin2bn(p_be, (int)p_len, NULL);
     int bits = BN_num_bits(p), width = (bits + 7) / 8, rc = 0, t;
     BIGNUM **alpha;
@@ -187,11 +296,12 @@ int hbo_encode(const unsigned char *p_be, size_t p_len, uint32_t sectors,
     enc_job_t *jobs;
     if (bits < 9 || sectors == 0) { BN_free(p); return -4; }
     alpha = (BIGNUM **)calloc(sectors, sizeof(BIGNUM *));
-    rc = prf_init(&a, a_key, keylen, p_be, p_len);
+    rc = prf_init_mode(&a, a_key, keylen, p_be, p_len, mode);
     if (rc) { BN_free(p); free(alpha); return rc; }
     for (uint32_t j = 0; j < sectors; j++) {                 /* alpha.eval(j), PySwizzle.py:302 */
-        alpha[j] = BN_new();
-        prf_eval(&a, j, alpha[j]);
+        alpha[j] = BN_new();                                 /* cxx: s.alpha(j), :681 */
+        if (mode) cxx_prf_eval(&a, j, alpha[j]);
+        else prf_eval(&a, j, alpha[j]);
     }
     prf_free(&a);
     if (nthreads < 1) nthreads = 1;
@@ -205,7 +315,7 @@ int hbo_encode(const unsigned char *p_be, size_t p_len, uint32_t sectors,
         J->block_base = block_base; J->data = data; J->len = len;
         J->b0 = nblocks * (uint64_t)t / (uint64_t)nthreads;
         J->b1 = nblocks * (uint64_t)(t + 1) / (uint64_t)nthreads;
-        J->tags = tags_out; J->width = width; J->alpha = alpha;
+        J->tags = tags_out; J->width = width; J->alpha = alpha; J->mode = mode;
         if (nthreads == 1) encode_worker(J);
         else pthread_create(&th[t], NULL, encode_worker, J);
     }

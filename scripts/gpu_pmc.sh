@@ -10,7 +10,7 @@ if [ -n "$LIST" ]; then timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1
 IFS=';' read -ra SETS <<< "$COUNTERS"
 i=0
 for mode in ${MODES:-two single}; do
-  extra=""; [ "$mode" = single ] && extra="--single-pass"
+  extra=""; [ "$mode" = single ] && extra="--single-pass"; [ "$mode" = cxx ] && extra="--prf cxx"
   for set in "${SETS[@]}"; do
     i=$((i+1))
     echo "== pass $i ($mode): $set"

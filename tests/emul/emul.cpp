@@ -241,3 +241,41 @@ extern "C" int emul_encode(const uint8_t *p_be, size_t plen, uint32_t S, const u
     if (bits <= 1024) return emul_encode_t<32>(p_be, plen, S, fkey, akey, keylen, block_base, data, len, nblocks, tags, lane, align, use_prefix);
     return -2;
 }
+
+// ------------------------------------------------------------------ cxx prf
+// One lane's cxx prf::evaluate (hb_cxx_try + SHA256(LE32)), as hb_engine<MODE 1>
+// runs it: tries until accepted or HB_CXX_MAX_TRIES.
+template <int NL>
+static int cxx_prf_eval(const LaneTab &L, const PrfParams<NL> &P, int nr, uint32_t x, uint32_t out[NL]) {
+    uint32_t dig[8], sr[4] = {0, 0, 0, 0};
+    hb_sha256_le32(x, dig);
+    for (uint32_t k = 1;; ++k) {
+        uint32_t ok = nr == 14 ? hb_cxx_try<NL, 14>(L, P, sr, dig, out)
+                    : nr == 12 ? hb_cxx_try<NL, 12>(L, P, sr, dig, out)
+                               : hb_cxx_try<NL, 10>(L, P, sr, dig, out);
+        if (ok || k >= HB_CXX_MAX_TRIES) return (int)k;
+    }
+}
+
+template <int NL>
+static int emul_cxx_prf_t(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen,
+                          uint32_t x, uint8_t *out_be, int lane) {
+    PrfParams<NL> P;
+    int nr;
+    if (!make_prf<NL>(key, keylen, range_be, rlen, P, nr)) return -1;
+    if (P.nb % 16) return -3;
+    LaneTab L = make_tab(lane);
+    uint32_t out[NL];
+    int tries = cxx_prf_eval<NL>(L, P, nr, x, out);
+    to_be(out, NL, out_be, P.nb);
+    return tries;
+}
+
+extern "C" int emul_cxx_prf(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen,
+                            uint32_t x, uint8_t *out_be, int lane) {
+    int bits = bitlen_be(range_be, rlen);
+    if (bits <= 256) return emul_cxx_prf_t<8>(key, keylen, range_be, rlen, x, out_be, lane);
+    if (bits <= 512) return emul_cxx_prf_t<16>(key, keylen, range_be, rlen, x, out_be, lane);
+    if (bits <= 1024) return emul_cxx_prf_t<32>(key, keylen, range_be, rlen, x, out_be, lane);
+    return -2;
+}

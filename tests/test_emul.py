@@ -72,3 +72,33 @@ def test_prefix_image_entries(emul, keylen):
     register bytes each entry stands for: all of P1, P2 and 4096 P3 entries."""
     key = bytes(range(7, 7 + keylen))
     assert emul.emul_prefix_check(key, keylen, 4096, 37) == 0
+
+
+CXX_LIMITS = [
+    int("db8709c32591ddc589b5c3c0986f92e0d11205b943c23a7e419e6c35b0256e6b", 16),  # bench prime
+    (1 << 255) + 95,          # E[tries] ~ 2: exercises retries
+    (1 << 127) + 45,          # 16-byte limit (one CFB block, truncated digest)
+    (1 << 384) - 317,         # 48 bytes: zero plaintext beyond the digest
+    (1 << 1023) + 1155,       # cxx API default width (1024-bit)
+    (17 << 1016) + 1,         # top byte 0x11: clz-derived mask 0x1f, many retries
+]
+
+
+def test_cxx_prf_lane_matches_oracle(emul):
+    """hb_cxx_try (full-output T-table AES, CFB-128, SHA256(LE32 i)) == the
+    oracle's OpenSSL restatement of cxx/prf.hxx (parity unpinned: no Crypto++)."""
+    import oracle.oracle as O
+    c = ctypes
+    emul.emul_cxx_prf.argtypes = [c.c_char_p, c.c_size_t, c.c_char_p, c.c_size_t, c.c_uint32,
+                                  c.c_char_p, c.c_int]
+    lane = 0
+    for keylen in (16, 24, 32):
+        key = bytes(range(3, 3 + keylen))
+        for lim in CXX_LIMITS:
+            nb = (lim.bit_length() + 7) // 8
+            for x in [0, 1, 2, 255, 256, 65537, 2 ** 31, 2 ** 32 - 1] + list(range(1000, 1040)):
+                out = ctypes.create_string_buffer(nb)
+                tries = emul.emul_cxx_prf(key, keylen, _be(lim), len(_be(lim)), x, out, lane % 64)
+                lane += 5
+                v, t = O.cxx_prf_eval(key, lim, x)
+                assert (int.from_bytes(out.raw, "big"), tries) == (v, t), (keylen, hex(lim), x)

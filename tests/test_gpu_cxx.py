@@ -1,0 +1,116 @@
+"""GPU parity of the cxx Swizzle mode (HB_PRF_CXX): the cxx extension's PRF
+(cxx/prf.hxx:125-176) and encode loop (cxx/shacham_waters_private.cxx:638-702)
+through the C ABI against the oracle's OpenSSL restatement of the same code.
+
+PARITY UNPINNED: Crypto++ (the reference's AES/SHA/Integer for this path) is
+absent here and no reference test pins cxx tag values, so these
+tests pin the HIP path to the oracle restatement only.  Bar: bit-exact.
+"""
+import ctypes
+import hashlib
+
+import pytest
+
+from test_gpu_parity import DevBuf, split_tags
+
+pytestmark = pytest.mark.gpu
+
+P256 = int("db8709c32591ddc589b5c3c0986f92e0d11205b943c23a7e419e6c35b0256e6b", 16)
+P1024 = int("c80499940aa92ecbb6d72ff89a2d3a5cdda832f9ee89ab5178e5947cf9395497ca08c737d6186a86004254e5"
+            "71f40d41c233faceebe0cd2b4176f31e89c7640e415dcf351863703a313ddb042f3868fdb2c690db3ddf6bca"
+            "562b5e8120a19824c11eec58e6c516c3ce3715556d52b88562a07368a6863dcc37ea43411b5150c7", 16)
+# limits of 16 / 32 / 48 / 128 bytes; E[tries] from ~1 to ~2; top byte 0x11 -> mask 0x1f
+LIMITS = [P256, (1 << 255) + 95, (1 << 127) + 45, (1 << 384) - 317, P1024, (1 << 1023) + 1155,
+          (17 << 1016) + 1]
+
+
+@pytest.fixture(scope="module")
+def nat():
+    from heartbeat_amd import _native
+    _native.context()
+    return _native
+
+
+def _be(n):
+    return n.to_bytes((n.bit_length() + 7) // 8, "big")
+
+
+@pytest.mark.parametrize("keylen", [16, 32])
+def test_cxx_prf_eval_vs_oracle(nat, oracle, keylen):
+    ctx = nat.context()
+    key = bytes(range(9, 9 + keylen))
+    xs = [0, 1, 2, 255, 256, 65537, 2 ** 31, 2 ** 32 - 1] + list(range(5000, 5300))
+    arr = (ctypes.c_uint32 * len(xs))(*xs)
+    for lim in LIMITS:
+        nb = (lim.bit_length() + 7) // 8
+        out = ctypes.create_string_buffer(nb * len(xs))
+        lb = _be(lim)
+        ctx.check(nat.lib().hb_cxx_prf_eval(ctx.h, key, keylen, lb, len(lb), arr, len(xs), out))
+        got = [int.from_bytes(out.raw[i * nb:(i + 1) * nb], "big") for i in range(len(xs))]
+        want = [oracle.cxx_prf_eval(key, lim, x)[0] for x in xs]
+        assert got == want, hex(lim)
+
+
+def test_cxx_prf_rejects_unaligned_limit(nat):
+    ctx = nat.context()
+    arr = (ctypes.c_uint32 * 1)(0)
+    out = ctypes.create_string_buffer(64)
+    lb = _be((1 << 250) + 1)          # 32 bytes: fine
+    assert nat.lib().hb_cxx_prf_eval(ctx.h, b"k" * 32, 32, lb, len(lb), arr, 1, out) == 0
+    lb = _be((1 << 200) + 1)          # 26 bytes: not a whole number of CFB-128 blocks
+    assert nat.lib().hb_cxx_prf_eval(ctx.h, b"k" * 32, 32, lb, len(lb), arr, 1, out) == nat.HB_EUNSUPPORTED
+
+
+def _cxx_encode_dev(nat, p, S, fk, ak, dptr, length, nblocks, tptr, block_base=0):
+    ctx = nat.context()
+    pb = _be(p)
+    ctx.check(nat.lib().hb_encode(ctx.h, pb, len(pb), S, fk, ak, len(fk), block_base, dptr, length,
+                                  nblocks, tptr, 3 | nat.HB_PRF_CXX, None))
+
+
+@pytest.mark.parametrize("p,S", [(P256, 16), (P256, 1), (P1024, 10), (P1024, 3)])
+def test_cxx_encode_edge_lengths_vs_oracle(nat, oracle, p, S):
+    ss = p.bit_length() // 8
+    C = ss * S
+    w = (p.bit_length() + 7) // 8
+    fk, ak = hashlib.sha256(b"cxx-f").digest(), hashlib.sha256(b"cxx-a").digest()
+    for L in [0, 1, ss - 1, ss, ss + 1, C - 1, C, C + 1, 3 * C + 17, 50 * C + 5]:
+        data = hashlib.sha256(b"d%d" % L).digest() * (L // 32 + 1)
+        data = data[:L]
+        nb = L // C + 1
+        buf = DevBuf(nat, max(L, 1))
+        tb = DevBuf(nat, nb * w)
+        try:
+            buf.upload(data)
+            _cxx_encode_dev(nat, p, S, fk, ak, buf.p, L, nb, tb.p)
+            assert split_tags(tb.download(), w) == oracle.cxx_encode(p, S, fk, ak, data), (L, S)
+        finally:
+            buf.free()
+            tb.free()
+
+
+def test_cxx_encode_64mib_vs_oracle(nat, oracle):
+    p, S = P256, 16
+    L = 64 << 20
+    nb = L // 512 + 1
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * 32)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 777))
+        fk, ak = hashlib.sha256(b"hb-bench-f").digest(), hashlib.sha256(b"hb-bench-alpha").digest()
+        _cxx_encode_dev(nat, p, S, fk, ak, buf.p, L, nb, tb.p)
+        want = oracle.cxx_encode(p, S, fk, ak, buf.download(), nthreads=16)
+        got = split_tags(tb.download(), 32)
+        assert got == want
+        # and the tags differ from PySwizzle's for the same keys (different PRF)
+        tp = DevBuf(nat, nb * 32)
+        try:
+            pb = _be(p)
+            ctx.check(nat.lib().hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, buf.p, L, nb, tp.p, 3, None))
+            assert split_tags(tp.download(), 32)[:100] != got[:100]
+        finally:
+            tp.free()
+    finally:
+        buf.free()
+        tb.free()
