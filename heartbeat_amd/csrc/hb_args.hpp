@@ -91,7 +91,9 @@ struct WsumArgs {
     u64 nterms;
     const unsigned char *data;
     u64 len, C;
-    u32 ss, S, tw, pad_;
+    u32 ss, S, tw;
+    u32 wrap32;                   // cxx prove: block offset = (unsigned int)(idx * C)
+                                  // (shacham_waters_private.cxx:738, 763)
     const unsigned char *tags;
     const u32 *vals;
     const u64 *blen;

@@ -111,7 +111,7 @@ struct HbPool {
 // hb_cxx_try), whose x is an unsigned int and which accepts after 81 tries.
 template <int MODE>
 __device__ __forceinline__ void hb_prf_digest(u64 x, u32 dig[8]) {
-    if (MODE == 1) hb_sha256_le32((u32)x, dig);
+    if (MODE != 0) hb_sha256_le32((u32)x, dig);
     else hb_sha256_decimal(x, dig);
 }
 
@@ -130,10 +130,11 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
     while (__ballot(active)) {
         u32 ok;
         if constexpr (MODE == 1) ok = hb_cxx_try<NL, NR>(L, P, sr, dig, out);
+        else if constexpr (MODE == 2) ok = hb_cxx_try_bytes<NL, NR>(L, P, sr, dig, out, job_tries);
         else ok = hb_prf_try<NL, NR>(L, P, sr, dig, out);
         tries += active ? 1u : 0u;
         job_tries += 1u;
-        if (MODE == 1 && job_tries >= HB_CXX_MAX_TRIES) ok = 1;   // `count++ < 80` (prf.hxx:142)
+        if (MODE != 0 && job_tries >= HB_CXX_MAX_TRIES) ok = 1;   // `count++ < 80` (prf.hxx:142)
         const bool acc = active && ok;
         if (acc) h.accept(job, out);
         // Exit guarantee: a job still rejected after HB_MAX_TRIES tries
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(256) void hb_wsum_kernel(WsumArgs<NL> A) {
             const u64 blk = gathered ? i : A.idx[i];
             if (col < A.S) {
                 const u64 blen = gathered ? A.blen[i] : A.len;
-                const u64 base = gathered ? i * A.C : blk * A.C;
+                const u64 base = gathered ? i * A.C : A.wrap32 ? (u64)(u32)(blk * A.C) : blk * A.C;
                 const u64 pos = base + (u64)col * A.ss;
                 const u64 end = gathered ? base + blen : A.len;
                 hb_sector_value<NL, ALIGN>(A.data, end, pos, A.ss, m);
@@ -501,7 +502,7 @@ hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass
 }
 
 
-// mode 0: KeyedPRF, 1: cxx prf
+// mode 0: KeyedPRF, 1: cxx prf (ByteCount(limit) % 16 == 0), 2: cxx prf (any limit)
 template <int NL>
 hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int mode, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
@@ -514,6 +515,8 @@ hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int mode, int grid, hipSt
     if (mode == 1) {
         if constexpr (NL >= 4) HB_PRF_NR(1);   // cxx limits are >= 16 bytes
         else return hipErrorInvalidValue;
+    } else if (mode == 2) {
+        HB_PRF_NR(2);
     } else {
         HB_PRF_NR(0);
     }

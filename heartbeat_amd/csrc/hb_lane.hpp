@@ -371,6 +371,50 @@ HB_HD u32 hb_cxx_try(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const 
     return borrow;
 }
 
+// One try of F' for any limit_sz (P.nb = ByteCount(limit) <= 4 NL, not
+// necessarily a multiple of 16: the cxx prove's indexer, limit = #tags).  The
+// stream continues across tries at byte granularity, so try `ntry` (0-based)
+// of an evaluation starts at byte (ntry * nb) mod 16 of the current CFB-128
+// block.  sr holds the register the way OpenSSL's CRYPTO_cfb128_encrypt keeps
+// ivec: at byte position 0 it is replaced by its encryption, then byte pos of
+// it is XORed with the plaintext and becomes the ciphertext byte.  With
+// nb % 16 == 0 this is hb_cxx_try.  Not on the encode hot path.
+template <int NL, int NR>
+HB_HD u32 hb_cxx_try_bytes(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], const u32 dig[8],
+                           u32 out[NL], u32 ntry) {
+    HB_UNROLL
+    for (int t = 0; t < NL; ++t) out[t] = 0;
+    u32 r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3];
+    const u32 nb = P.nb;
+    u32 pos = (ntry * nb) & 15u;
+    HB_NOUNROLL
+    for (u32 b = 0; b < nb; ++b) {
+        if (pos == 0) hb_aes_full<NR>(L, P.rk, r0, r1, r2, r3);
+        // plaintext byte b of dig || 0... (dig holds big-endian words)
+        const u32 pt = b < 32 ? (dig[b >> 2] >> (24 - 8 * (b & 3))) & 0xffu : 0u;
+        const u32 sh = 8 * (pos & 3), wsel = pos >> 2;
+        const u32 x = (pt << sh);
+        r0 ^= wsel == 0 ? x : 0u; r1 ^= wsel == 1 ? x : 0u;
+        r2 ^= wsel == 2 ? x : 0u; r3 ^= wsel == 3 ? x : 0u;
+        const u32 w = wsel == 0 ? r0 : wsel == 1 ? r1 : wsel == 2 ? r2 : r3;
+        u32 cb = (w >> sh) & 0xffu;
+        if (b == 0) cb &= P.topmask;
+        // ciphertext byte b is byte nb-1-b of the big-endian result
+        const u32 at = nb - 1 - b, ti = at >> 2, tsh = 8 * (at & 3);
+        HB_UNROLL
+        for (int t = 0; t < NL; ++t) out[t] |= (u32)t == ti ? cb << tsh : 0u;
+        pos = (pos + 1) & 15u;
+    }
+    sr[0] = r0; sr[1] = r1; sr[2] = r2; sr[3] = r3;
+    u32 borrow = 0;
+    HB_UNROLL
+    for (int t = 0; t < NL; ++t) {
+        u64 d = (u64)out[t] - (u64)P.R[t] - (u64)borrow;
+        borrow = (u32)(d >> 63);
+    }
+    return borrow;
+}
+
 // ------------------------------------------------------------------ CFB prefix
 // Every eval starts a fresh cipher with IV = 0 (util.py:88), so the first four
 // AES inputs of the first try are 0^16, 0^15 c0, 0^14 c0 c1 and 0^13 c0 c1 c2:

@@ -425,6 +425,14 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     Limbs p = from_be(p_be, p_len, NL);
     const u64 C = (u64)pi.ss * S;
     const u32 ncols = S + 1;
+    // cxx prove (shacham_waters_private.cxx:731-789): a challenge of at least
+    // #tags chunks checks every block in order without the index PRF
+    // (check_all, :754-755, 762); both PRFs are the cxx prf; block offsets are
+    // computed in unsigned int (index*chunk_size, :738, 763).
+    const bool cxx = flags & HB_PRF_CXX;
+    const bool check_all = cxx && chunks >= ntags;
+    if (check_all) chunks = ntags;
+    if (cxx && (ntags >> 32)) return fail(c, HB_EUNSUPPORTED, "cxx prove: more than 2^32 - 1 tags");
     if (chunks == 0) {
         memset(mu_out, 0, (size_t)S * pi.tw);
         memset(sigma_out, 0, pi.tw);
@@ -436,10 +444,31 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     HB_CHECK(c->idx.ensure((size_t)chunks * 8), "hipMalloc(idx)");
     HB_CHECK(c->vals.ensure((size_t)chunks * NL * 4), "hipMalloc(v)");
     HB_CHECK(c->wts.ensure((size_t)chunks * NL * 4), "hipMalloc(w)");
-    int rc = run_prf<2>(c, chal_key, key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 2);
+    int rc = 0;
+    if (check_all) {
+        std::vector<u64> iota(chunks);
+        for (u64 i = 0; i < chunks; ++i) iota[i] = i;
+        HB_CHECK(hipMemcpyAsync(c->idx.p, iota.data(), (size_t)chunks * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+        HB_CHECK(hipStreamSynchronize(c->stream), "H2D(idx)");
+    } else {
+        // cxx indexer: limit = #tags, a few bytes -> byte-granular CFB-128 (mode 2)
+        rc = run_prf<2>(c, chal_key, key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 2, cxx ? 2 : 0);
+        if (rc) return rc;
+    }
+    const int vnb = (bitlen_be(vmax_be, vmax_len) + 7) / 8;
+    rc = run_prf<NL>(c, chal_key, key_len, vmax_be, vmax_len, nullptr, 0, chunks, (u32 *)c->vals.p, 3,
+                     cxx ? (vnb % 16 ? 2 : 1) : 0);
     if (rc) return rc;
-    rc = run_prf<NL>(c, chal_key, key_len, vmax_be, vmax_len, nullptr, 0, chunks, (u32 *)c->vals.p, 3);
-    if (rc) return rc;
+    if (cxx && !check_all) {
+        // after 81 rejected tries the cxx prf returns a value >= the limit
+        // (prf.hxx:142); the reference's t.sigma().at(index) then throws
+        std::vector<u64> hidx(chunks);
+        HB_CHECK(hipMemcpyAsync(hidx.data(), c->idx.p, (size_t)chunks * 8, hipMemcpyDeviceToHost, c->stream),
+                 "hipMemcpy(idx)");
+        HB_CHECK(hipStreamSynchronize(c->stream), "prf");
+        for (u64 i = 0; i < chunks; ++i)
+            if (hidx[i] >= ntags) return fail(c, HB_EINVAL, "vector::_M_range_check: challenge index out of range");
+    }
     rc = run_mont<NL>(c, p, (const u32 *)c->vals.p, (u32 *)c->wts.p, chunks);
     if (rc) return rc;
 
@@ -454,6 +483,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     A.ss = pi.ss;
     A.S = S;
     A.tw = pi.tw;
+    A.wrap32 = cxx ? 1u : 0u;
     const u32 gx = wsum_grid(chunks);
     const u32 nparts = gx * 256;
     HB_CHECK(c->partials.ensure((size_t)ncols * nparts * NL * 4), "hipMalloc(partials)");
@@ -487,7 +517,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         for (u64 i = 0; i < chunks; ++i) {
             const u64 ix = hidx[i];
             if (ix >= ntags) return fail(c, HB_EINVAL, "internal: index out of range");
-            const u64 off = ix * C;
+            const u64 off = cxx ? (u64)(u32)(ix * C) : ix * C;
             const u64 n = off >= len ? 0 : (len - off < C ? len - off : C);
             blen[i] = n;
             if (n) {
@@ -713,7 +743,7 @@ int hb_cxx_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t
     const int nl = nl_for_bits(bits);
     const size_t nb = (size_t)(bits + 7) / 8;
     if (!nl) return fail(c, HB_EUNSUPPORTED, "PRF limits above 1024 bits are not supported by this build");
-    if (nb % 16) return fail(c, HB_EUNSUPPORTED, "cxx prf mode needs ByteCount(limit) to be a multiple of 16");
+    const int mode = nb % 16 ? 2 : 1;   // byte-granular CFB-128 unless whole blocks per try
     if (n == 0) return 0;
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     std::vector<u64> x64(n);
@@ -724,9 +754,9 @@ int hb_cxx_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t
     HB_CHECK(hipMemcpyAsync(c->xs.p, x64.data(), n * 8, hipMemcpyHostToDevice, c->stream), "H2D");
     int rc = 0;
     switch (nlv) {
-    case 8: rc = run_prf<8>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, 1); break;
-    case 16: rc = run_prf<16>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, 1); break;
-    default: rc = run_prf<32>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, 1); break;
+    case 8: rc = run_prf<8>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
+    case 16: rc = run_prf<16>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
+    default: rc = run_prf<32>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
     }
     if (rc) return rc;
     std::vector<u32> h(n * (size_t)nlv);

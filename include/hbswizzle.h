@@ -103,8 +103,10 @@ int hb_encode(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
               uint64_t *tries_out);
 
 /* The cxx prf, prf::evaluate(i) (cxx/prf.hxx:125-145), for n unsigned-int
- * inputs, keyed by key and bounded by limit (ByteCount(limit) % 16 == 0):
- * out receives n values of ByteCount(limit) big-endian bytes each. */
+ * inputs, keyed by key and bounded by limit (any limit up to 1024 bits; when
+ * ByteCount(limit) is not a multiple of 16 the CFB-128 stream continues
+ * mid-block across tries): out receives n values of ByteCount(limit)
+ * big-endian bytes each. */
 int hb_cxx_prf_eval(hb_ctx *ctx, const uint8_t *key, size_t key_len,
                     const uint8_t *limit_be, size_t limit_len,
                     const uint32_t *xs, size_t n, uint8_t *out);
@@ -120,7 +122,12 @@ uint64_t hb_block_count(const uint8_t *p_be, size_t p_len, uint32_t sectors,
  *   mu_j  = sum_i v_i * m_{idx_i, j} mod p      (i < chunks)
  *   sigma = sum_i v_i * tags[idx_i]    mod p
  * tags: ntags * hb_width(p) bytes.  data: the whole file (len bytes).
- * mu_out: sectors * hb_width(p) bytes, sigma_out: hb_width(p) bytes (host). */
+ * mu_out: sectors * hb_width(p) bytes, sigma_out: hb_width(p) bytes (host).
+ * With HB_PRF_CXX: the cxx extension's prove (shacham_waters_private.cxx:731-789)
+ * -- idx_i and v_i from the cxx prf (cxx/prf.hxx), every block in order when
+ * chunks >= ntags (check_all, :754-762), and block offsets computed as
+ * (unsigned int)(idx * sectors * ss) like the reference (:738, 763; differs
+ * from PySwizzle for blocks past 4 GiB).  Parity unpinned (Crypto++ absent). */
 int hb_prove(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
              const uint8_t *chal_key, size_t key_len, uint64_t chunks,
              const uint8_t *vmax_be, size_t vmax_len,

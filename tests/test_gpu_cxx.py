@@ -51,14 +51,109 @@ def test_cxx_prf_eval_vs_oracle(nat, oracle, keylen):
         assert got == want, hex(lim)
 
 
-def test_cxx_prf_rejects_unaligned_limit(nat):
+# limits whose ByteCount is not a multiple of 16 (the cxx prove's indexer has
+# limit = #tags): the CFB-128 stream continues mid-block across tries
+SMALL_LIMITS = [2, 255, 256, 10000, (1 << 27) + 1, 9437185, (1 << 32) - 5, (1 << 200) + 1,
+                (17 << 120) + 3]
+
+
+def test_cxx_prf_small_limits_vs_oracle(nat, oracle):
     ctx = nat.context()
-    arr = (ctypes.c_uint32 * 1)(0)
-    out = ctypes.create_string_buffer(64)
-    lb = _be((1 << 250) + 1)          # 32 bytes: fine
-    assert nat.lib().hb_cxx_prf_eval(ctx.h, b"k" * 32, 32, lb, len(lb), arr, 1, out) == 0
-    lb = _be((1 << 200) + 1)          # 26 bytes: not a whole number of CFB-128 blocks
-    assert nat.lib().hb_cxx_prf_eval(ctx.h, b"k" * 32, 32, lb, len(lb), arr, 1, out) == nat.HB_EUNSUPPORTED
+    key = hashlib.sha256(b"hb-bench-chal").digest()
+    xs = list(range(400)) + [2 ** 32 - 1]
+    arr = (ctypes.c_uint32 * len(xs))(*xs)
+    for lim in SMALL_LIMITS:
+        nb = (lim.bit_length() + 7) // 8
+        out = ctypes.create_string_buffer(nb * len(xs))
+        lb = _be(lim)
+        ctx.check(nat.lib().hb_cxx_prf_eval(ctx.h, key, 32, lb, len(lb), arr, len(xs), out))
+        got = [int.from_bytes(out.raw[i * nb:(i + 1) * nb], "big") for i in range(len(xs))]
+        want = [oracle.cxx_prf_eval(key, lim, x)[0] for x in xs]
+        assert got == want, hex(lim)
+
+
+def _cxx_prove_want(oracle, p, S, key, chunks, vmax, ntags, tags, read):
+    """shacham_waters_private::prove (cxx/shacham_waters_private.cxx:731-789)
+    restated over the oracle's cxx prf: check_all when chunks >= #tags, block
+    offsets in unsigned int (:738, 763), duplicate indices counted again."""
+    ss = p.bit_length() // 8
+    C = S * ss
+    check_all = chunks >= ntags
+    n = ntags if check_all else chunks
+    mu = [0] * S
+    sigma = 0
+    for i in range(n):
+        idx = i if check_all else oracle.cxx_prf_eval(key, ntags, i)[0]
+        v = oracle.cxx_prf_eval(key, vmax, i)[0]
+        off = (idx * C) & 0xffffffff
+        for j in range(S):
+            mu[j] = (mu[j] + v * int.from_bytes(read(off + j * ss, ss), "big")) % p
+        sigma = (sigma + v * tags(idx)) % p
+    return mu, sigma
+
+
+def _cxx_prove_dev(nat, p, S, key, chunks, vmax, tptr, ntags, dptr, L):
+    ctx = nat.context()
+    w = (p.bit_length() + 7) // 8
+    mu = ctypes.create_string_buffer(w * S)
+    sg = ctypes.create_string_buffer(w)
+    pb, vb = _be(p), _be(vmax)
+    ctx.check(nat.lib().hb_prove(ctx.h, pb, len(pb), S, key, len(key), chunks, vb, len(vb), tptr, ntags,
+                                 dptr, L, 3 | nat.HB_PRF_CXX, mu, sg))
+    return [int.from_bytes(mu.raw[j * w:(j + 1) * w], "big") for j in range(S)], int.from_bytes(sg.raw, "big")
+
+
+@pytest.mark.parametrize("chunks", [0, 1, 257, 1000, 5000])
+def test_cxx_prove_vs_oracle(nat, oracle, chunks):
+    """Small file (1000 tags at S = 16): sampled challenges and, for
+    chunks >= #tags, the check_all path."""
+    p, S = P256, 16
+    L = 1000 * 512 - 100
+    ntags = L // 512 + 1
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, ntags * 32)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 31))
+        fk, ak = hashlib.sha256(b"cxx-f").digest(), hashlib.sha256(b"cxx-a").digest()
+        _cxx_encode_dev(nat, p, S, fk, ak, buf.p, L, ntags, tb.p)
+        data, traw = buf.download(), tb.download()
+        key = hashlib.sha256(b"hb-bench-chal").digest()
+        got = _cxx_prove_dev(nat, p, S, key, chunks, p, tb.p, ntags, buf.p, L)
+        want = _cxx_prove_want(oracle, p, S, key, chunks, p, ntags,
+                               lambda k: int.from_bytes(traw[k * 32:(k + 1) * 32], "big"),
+                               lambda off, n: data[off:off + n])
+        assert got == want
+    finally:
+        buf.free()
+        tb.free()
+
+
+def test_cxx_prove_offsets_wrap_at_4gib(nat, oracle):
+    """A 4.5 GiB device-resident file: challenged blocks past 4 GiB are read at
+    (index * chunk_size) mod 2^32, as the reference's unsigned int arithmetic
+    does (shacham_waters_private.cxx:738, 763)."""
+    p, S = P256, 16
+    L = 9 << 29
+    ntags = L // 512 + 1
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, ntags * 32)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 4))
+        ctx.check(nat.lib().hb_fill_random(ctx.h, tb.p, ntags * 32, 5))   # tags: any values
+        key = hashlib.sha256(b"wrap").digest()
+        chunks = 200
+        idx = [oracle.cxx_prf_eval(key, ntags, i)[0] for i in range(chunks)]
+        assert sum(k * 512 >= 1 << 32 for k in idx) > 10
+        got = _cxx_prove_dev(nat, p, S, key, chunks, p, tb.p, ntags, buf.p, L)
+        want = _cxx_prove_want(oracle, p, S, key, chunks, p, ntags,
+                               lambda k: int.from_bytes(tb.download(32, k * 32), "big"),
+                               lambda off, n: buf.download(max(0, min(n, L - off)), off))
+        assert got == want
+    finally:
+        buf.free()
+        tb.free()
 
 
 def _cxx_encode_dev(nat, p, S, fk, ak, dptr, length, nblocks, tptr, block_base=0):
