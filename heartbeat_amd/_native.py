@@ -46,6 +46,9 @@ SIGNATURES = [
     ("hb_verify_rhs", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _B, _c.c_size_t,
                                  _c.c_uint64, _B, _c.c_size_t, _c.c_uint64, _B, _c.c_size_t,
                                  _B, _P]),
+    ("hb_cxx_verify_rhs", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _B, _c.c_size_t,
+                                     _c.c_uint64, _B, _c.c_size_t, _c.c_uint64, _B, _c.c_size_t,
+                                     _B, _P]),
     ("hb_aes_cfb8", _c.c_int, [_B, _c.c_size_t, _B, _B, _P, _c.c_size_t, _c.c_int]),
     ("hb_last_kernel_ms", _c.c_int, [_P, _c.POINTER(_c.c_double), _c.POINTER(_c.c_uint32)]),
     ("hb_device_malloc", _c.c_int, [_P, _c.c_uint64, _c.POINTER(_P)]),

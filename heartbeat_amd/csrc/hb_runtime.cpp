@@ -570,8 +570,14 @@ template <int NL>
 int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
                 const uint8_t *f_key, const uint8_t *a_key, size_t key_len, u64 state_chunks,
                 const uint8_t *chal_key, size_t chal_key_len, u64 chunks, const uint8_t *vmax_be,
-                size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out) {
+                size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out, bool cxx = false) {
     Limbs p = from_be(p_be, p_len, NL);
+    // cxx verify (shacham_waters_private.cxx:791-842): cxx prf throughout,
+    // check_all when the challenge covers every block (:822-827)
+    const bool check_all = cxx && chunks >= state_chunks;
+    if (check_all) chunks = state_chunks;
+    const int pmode = cxx ? (pi.tw % 16 ? 2 : 1) : 0;
+    const int vmode = cxx ? ((bitlen_be(vmax_be, vmax_len) + 7) / 8 % 16 ? 2 : 1) : 0;
     const u64 nterms = chunks + S;
     uint8_t nbe[8];
     u64_be(state_chunks, nbe);
@@ -583,16 +589,23 @@ int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     int rc = 0;
     if (chunks) {
         // index = KeyedPRF(key, state.chunks), v = KeyedPRF(key, v_max)   (PySwizzle.py:381-382)
-        rc = run_prf<2>(c, chal_key, chal_key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 2);
-        if (rc) return rc;
-        rc = run_prf<NL>(c, chal_key, chal_key_len, vmax_be, vmax_len, nullptr, 0, chunks, raw, 3);
+        if (check_all) {
+            std::vector<u64> iota(chunks);
+            for (u64 i = 0; i < chunks; ++i) iota[i] = i;
+            HB_CHECK(hipMemcpyAsync(c->idx.p, iota.data(), (size_t)chunks * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+            HB_CHECK(hipStreamSynchronize(c->stream), "H2D(idx)");
+        } else {
+            rc = run_prf<2>(c, chal_key, chal_key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 2, cxx ? 2 : 0);
+            if (rc) return rc;
+        }
+        rc = run_prf<NL>(c, chal_key, chal_key_len, vmax_be, vmax_len, nullptr, 0, chunks, raw, 3, vmode);
         if (rc) return rc;
         // f.eval(index.eval(i))   (PySwizzle.py:389)
-        rc = run_prf<NL>(c, f_key, key_len, p_be, p_len, (const u64 *)c->idx.p, 0, chunks, val, 4);
+        rc = run_prf<NL>(c, f_key, key_len, p_be, p_len, (const u64 *)c->idx.p, 0, chunks, val, 4, pmode);
         if (rc) return rc;
     }
     // alpha.eval(j)   (PySwizzle.py:392)
-    rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, raw + chunks * NL, 5);
+    rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, raw + chunks * NL, 5, pmode);
     if (rc) return rc;
     rc = run_mont<NL>(c, p, raw, w, nterms);
     if (rc) return rc;
@@ -809,10 +822,34 @@ int hb_prove(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
     }
 }
 
+static int verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                      const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
+                      uint64_t state_chunks, const uint8_t *chal_key, size_t chal_key_len, uint64_t chunks,
+                      const uint8_t *vmax_be, size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out, bool cxx);
+
 int hb_verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
                   const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
                   uint64_t state_chunks, const uint8_t *chal_key, size_t chal_key_len, uint64_t chunks,
                   const uint8_t *vmax_be, size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out) {
+    return verify_rhs(c, p_be, p_len, sectors, f_key, alpha_key, key_len, state_chunks, chal_key,
+                      chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, false);
+}
+
+int hb_cxx_verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                      const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
+                      uint64_t state_chunks, const uint8_t *chal_key, size_t chal_key_len, uint64_t chunks,
+                      const uint8_t *vmax_be, size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out) {
+    if (c && (state_chunks >> 32)) return fail(c, HB_EUNSUPPORTED, "cxx verify: more than 2^32 - 1 blocks");
+    return verify_rhs(c, p_be, p_len, sectors, f_key, alpha_key, key_len, state_chunks, chal_key,
+                      chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, true);
+}
+
+}  // extern "C"
+
+static int verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                      const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
+                      uint64_t state_chunks, const uint8_t *chal_key, size_t chal_key_len, uint64_t chunks,
+                      const uint8_t *vmax_be, size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out, bool cxx) {
     if (!c) return HB_EINVAL;
     PrimeInfo pi;
     if (int rc = parse_prime(c, p_be, p_len, pi)) return rc;
@@ -825,11 +862,13 @@ int hb_verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors
     if (vbits > 32 * pi.nl) return fail(c, HB_EUNSUPPORTED, "v_max wider than the prime's limb count");
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     switch (pi.nl) {
-    case 8: return verify_impl<8>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out);
-    case 16: return verify_impl<16>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out);
-    default: return verify_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out);
+    case 8: return verify_impl<8>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
+    case 16: return verify_impl<16>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
+    default: return verify_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
     }
 }
+
+extern "C" {
 
 int hb_aes_cfb8(const uint8_t *key, size_t key_len, const uint8_t *iv, const uint8_t *in,
                 uint8_t *out, size_t n, int encrypt) {

@@ -146,6 +146,17 @@ int hb_verify_rhs(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t secto
                   const uint8_t *vmax_be, size_t vmax_len,
                   const uint8_t *mu, uint8_t *rhs_out);
 
+/* Right-hand side of the cxx extension's verify (shacham_waters_private.cxx:
+ * 791-842) for a decrypted state: the same sum as hb_verify_rhs with the cxx
+ * prf (cxx/prf.hxx) for index, v, f and alpha, and every block in order when
+ * chunks >= state_chunks (check_all, :822-827).  Parity unpinned. */
+int hb_cxx_verify_rhs(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                      const uint8_t *f_key, const uint8_t *alpha_key, size_t key_len,
+                      uint64_t state_chunks,
+                      const uint8_t *chal_key, size_t chal_key_len, uint64_t chunks,
+                      const uint8_t *vmax_be, size_t vmax_len,
+                      const uint8_t *mu, uint8_t *rhs_out);
+
 /* Host AES-CFB8 (segment 8, any 16-byte IV) for PySwizzle State
  * encrypt/decrypt (PySwizzle.py:162-195): 64 bytes per call, not a hot path.
  * encrypt = 1 encrypts, 0 decrypts. */

@@ -1,0 +1,71 @@
+"""heartbeat_amd.Swizzle, the cxx extension's scheme object (cxx/Swizzle.hxx,
+cxx/shacham_waters_private.cxx:638-842), through the GPU cxx mode.  Flows
+follow the reference's tests/tests_unit_swpriv.py (round trips, public copies,
+tampered files, serialisation); values are checked against the oracle's cxx
+restatement.  Parity unpinned (Crypto++ absent).
+"""
+import hashlib
+import io
+
+import pytest
+
+from test_gpu_cxx import P1024, _cxx_prove_want
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sw():
+    from heartbeat_amd import Swizzle as m
+    return m
+
+
+DATA = b"".join(hashlib.sha256(b"swz%d" % i).digest() for i in range(400)) + b"tail!"
+
+
+@pytest.mark.parametrize("frac", [1.0, 0.3])
+def test_round_trip(sw, oracle, frac):
+    beat = sw.Swizzle(frac, 10, prime=P1024)
+    tag, state = beat.encode(io.BytesIO(DATA))
+    assert len(tag) == len(DATA) // (10 * 128) + 1
+    # tags are the cxx encode of the state's keys
+    st = sw.State.fromdict(state.todict())
+    st.decrypt(beat.k_enc)
+    assert tag.sigma == oracle.cxx_encode(P1024, 10, st.f_key, st.alpha_key, DATA)
+    chal = beat.gen_challenge(state)
+    assert chal.chunks == int(frac * len(tag))
+    proof = beat.get_public().prove(io.BytesIO(DATA), chal, tag)
+    want = _cxx_prove_want(oracle, P1024, 10, chal.key, chal.chunks, P1024, len(tag),
+                           lambda k: tag.sigma[k], lambda off, n: DATA[off:off + n])
+    assert (proof.mu, proof.sigma) == want
+    assert beat.verify(proof, chal, state)
+    # state untouched by gen_challenge / verify (the reference copies it)
+    assert state.encrypted
+
+
+def test_tampered_file_fails(sw):
+    beat = sw.Swizzle(1.0, 10, prime=P1024)
+    tag, state = beat.encode(io.BytesIO(DATA))
+    chal = beat.gen_challenge(state)
+    bad = bytearray(DATA)
+    bad[1000] ^= 1
+    proof = beat.prove(io.BytesIO(bytes(bad)), chal, tag)
+    assert not beat.verify(proof, chal, state)
+
+
+def test_wrong_key_and_mu_length(sw):
+    beat = sw.Swizzle(1.0, 10, prime=P1024)
+    tag, state = beat.encode(io.BytesIO(DATA))
+    chal = beat.gen_challenge(state)
+    proof = beat.prove(io.BytesIO(DATA), chal, tag)
+    other = sw.Swizzle(1.0, 10, prime=P1024)
+    assert not other.verify(proof, chal, state)          # state does not decrypt
+    proof.mu = proof.mu[:-1]
+    assert not beat.verify(proof, chal, state)           # p.mu().size() != _sectors
+
+
+def test_serialisation(sw):
+    beat = sw.Swizzle(0.5, 7, prime=P1024)
+    assert sw.Swizzle.fromdict(beat.todict()) == beat
+    pub = beat.get_public()
+    assert pub.public and pub.k_enc == b"\0" * 32 and pub != beat
