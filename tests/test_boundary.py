@@ -137,3 +137,7 @@ def test_no_gpu_fails_loudly():
     beat = PySwizzle(4, b"k" * 32, prime=(1 << 256) - 189)
     with pytest.raises(HeartbeatError):
         beat.encode(io.BytesIO(b"hello"))
+    from heartbeat_amd.Swizzle import Swizzle
+    sw = Swizzle(1.0, 4, prime=(1 << 256) - 189)
+    with pytest.raises(HeartbeatError):
+        sw.encode(io.BytesIO(b"hello"))
