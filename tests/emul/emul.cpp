@@ -244,15 +244,22 @@ extern "C" int emul_encode(const uint8_t *p_be, size_t plen, uint32_t S, const u
 
 // ------------------------------------------------------------------ cxx prf
 // One lane's cxx prf::evaluate (hb_cxx_try + SHA256(LE32)), as hb_engine<MODE 1>
-// runs it: tries until accepted or HB_CXX_MAX_TRIES.
+// runs it -- or hb_cxx_try_bytes (MODE 2) when ByteCount(limit) % 16 != 0:
+// tries until accepted or HB_CXX_MAX_TRIES.
 template <int NL>
 static int cxx_prf_eval(const LaneTab &L, const PrfParams<NL> &P, int nr, uint32_t x, uint32_t out[NL]) {
     uint32_t dig[8], sr[4] = {0, 0, 0, 0};
     hb_sha256_le32(x, dig);
     for (uint32_t k = 1;; ++k) {
-        uint32_t ok = nr == 14 ? hb_cxx_try<NL, 14>(L, P, sr, dig, out)
-                    : nr == 12 ? hb_cxx_try<NL, 12>(L, P, sr, dig, out)
-                               : hb_cxx_try<NL, 10>(L, P, sr, dig, out);
+        uint32_t ok;
+        if (P.nb % 16)
+            ok = nr == 14 ? hb_cxx_try_bytes<NL, 14>(L, P, sr, dig, out, k - 1)
+               : nr == 12 ? hb_cxx_try_bytes<NL, 12>(L, P, sr, dig, out, k - 1)
+                          : hb_cxx_try_bytes<NL, 10>(L, P, sr, dig, out, k - 1);
+        else
+            ok = nr == 14 ? hb_cxx_try<NL, 14>(L, P, sr, dig, out)
+               : nr == 12 ? hb_cxx_try<NL, 12>(L, P, sr, dig, out)
+                          : hb_cxx_try<NL, 10>(L, P, sr, dig, out);
         if (ok || k >= HB_CXX_MAX_TRIES) return (int)k;
     }
 }
@@ -263,7 +270,6 @@ static int emul_cxx_prf_t(const uint8_t *key, size_t keylen, const uint8_t *rang
     PrfParams<NL> P;
     int nr;
     if (!make_prf<NL>(key, keylen, range_be, rlen, P, nr)) return -1;
-    if (P.nb % 16) return -3;
     LaneTab L = make_tab(lane);
     uint32_t out[NL];
     int tries = cxx_prf_eval<NL>(L, P, nr, x, out);

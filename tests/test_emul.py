@@ -81,11 +81,14 @@ CXX_LIMITS = [
     (1 << 384) - 317,         # 48 bytes: zero plaintext beyond the digest
     (1 << 1023) + 1155,       # cxx API default width (1024-bit)
     (17 << 1016) + 1,         # top byte 0x11: clz-derived mask 0x1f, many retries
+    # ByteCount not a multiple of 16 (hb_cxx_try_bytes; the cxx prove's
+    # indexer has limit = #tags): the CFB-128 stream continues mid-block
+    2, 255, 10000, (1 << 27) + 1, 9437185, (1 << 200) + 1, (17 << 120) + 3,
 ]
 
 
 def test_cxx_prf_lane_matches_oracle(emul):
-    """hb_cxx_try (full-output T-table AES, CFB-128, SHA256(LE32 i)) == the
+    """hb_cxx_try / hb_cxx_try_bytes (full-output T-table AES, CFB-128, SHA256(LE32 i)) == the
     oracle's OpenSSL restatement of cxx/prf.hxx (parity unpinned: no Crypto++)."""
     import oracle.oracle as O
     c = ctypes
