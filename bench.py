@@ -252,7 +252,11 @@ def bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak
     gathered weighted sums of the S sector columns and of the tags, and the
     mod-p reductions, with mu and sigma copied back to the host."""
     chunks = cfg["prove_chunks"]
-    ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, dptr, length, nblocks, tptr, 3, None))
+    # --prf cxx: the cxx extension's prove (shacham_waters_private.cxx:731-789)
+    from heartbeat_amd import _native
+    cxx = args.prf == "cxx"
+    pflags = 3 | (_native.HB_PRF_CXX if cxx else 0)
+    ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, dptr, length, nblocks, tptr, pflags, None))
     ck = hashlib.sha256(b"hb-bench-challenge").digest()
     vb = pb                                   # v_max = p, as gen_challenge (PySwizzle.py:329)
     w = 32
@@ -261,7 +265,7 @@ def bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak
 
     def step():
         ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, ck, len(ck), chunks, vb, len(vb), tptr, nblocks,
-                             dptr, length, 3, mu, sg))
+                             dptr, length, pflags, mu, sg))
 
     for _ in range(max(1, args.warmup)):
         step()
@@ -277,10 +281,11 @@ def bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak
         "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (SplitMix64 random file bytes, seeded keys)",
         "config": {"workload": cfg["name"], "file_bytes": length, "blocks_total": nblocks,
-                   "sectors": S, "prime_bits": 256, "chunks": chunks},
+                   "sectors": S, "prime_bits": 256, "chunks": chunks,
+                   "prf": "cxx prf, cxx prove (parity unpinned)" if cxx else "PySwizzle KeyedPRF"},
         "gathered_bytes_per_proof": chunks * (C + w),
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and not cxx:
         import numpy as np
         from oracle import oracle as O
         host = np.empty(length, dtype=np.uint8)
