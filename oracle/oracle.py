@@ -127,6 +127,32 @@ def cxx_encode(p, sectors, f_key, alpha_key, data, block_base=0, nblocks=None, n
     return encode(p, sectors, f_key, alpha_key, data, block_base, nblocks, nthreads, _fn="hbo_cxx_encode")
 
 
+def cxx_prove(p, sectors, chal_key, chunks, v_max, ntags, tag_at, read_at):
+    """(mu list, sigma) of the cxx shacham_waters_private::prove
+    (cxx/shacham_waters_private.cxx:731-789) over cxx_prf_eval: every block in
+    order when chunks >= #tags (check_all, :754-755, 762), else
+    idx_i = prf(key, #tags)(i) (:743-744, 762); v_i = prf(key, v_max)(i)
+    (:746-748, 767); block offset (unsigned int)(index * chunk_size) (:738, 763);
+    duplicate indices count again.  tag_at(k) -> int, read_at(off, n) -> the
+    file bytes [off, off + n) clipped at EOF (a seek past EOF reads nothing).
+    Parity unpinned (Crypto++ absent)."""
+    p = int(p)
+    ss = p.bit_length() // 8
+    C = sectors * ss
+    check_all = chunks >= ntags
+    n = ntags if check_all else chunks
+    mu = [0] * sectors
+    sigma = 0
+    for i in range(n):
+        idx = i if check_all else cxx_prf_eval(chal_key, ntags, i)[0]
+        v = cxx_prf_eval(chal_key, v_max, i)[0]
+        off = (idx * C) & 0xffffffff
+        for j in range(sectors):
+            mu[j] = (mu[j] + v * int.from_bytes(read_at(off + j * ss, ss), "big")) % p
+        sigma = (sigma + v * tag_at(idx)) % p
+    return mu, sigma
+
+
 def prove(p, sectors, chal_key, chunks, v_max, tags, data):
     """(mu list, sigma) of PySwizzle.prove."""
     p = int(p)

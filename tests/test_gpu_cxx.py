@@ -73,23 +73,8 @@ def test_cxx_prf_small_limits_vs_oracle(nat, oracle):
 
 
 def _cxx_prove_want(oracle, p, S, key, chunks, vmax, ntags, tags, read):
-    """shacham_waters_private::prove (cxx/shacham_waters_private.cxx:731-789)
-    restated over the oracle's cxx prf: check_all when chunks >= #tags, block
-    offsets in unsigned int (:738, 763), duplicate indices counted again."""
-    ss = p.bit_length() // 8
-    C = S * ss
-    check_all = chunks >= ntags
-    n = ntags if check_all else chunks
-    mu = [0] * S
-    sigma = 0
-    for i in range(n):
-        idx = i if check_all else oracle.cxx_prf_eval(key, ntags, i)[0]
-        v = oracle.cxx_prf_eval(key, vmax, i)[0]
-        off = (idx * C) & 0xffffffff
-        for j in range(S):
-            mu[j] = (mu[j] + v * int.from_bytes(read(off + j * ss, ss), "big")) % p
-        sigma = (sigma + v * tags(idx)) % p
-    return mu, sigma
+    """The oracle's restatement of shacham_waters_private::prove (oracle.cxx_prove)."""
+    return oracle.cxx_prove(p, S, key, chunks, vmax, ntags, tags, read)
 
 
 def _cxx_prove_dev(nat, p, S, key, chunks, vmax, tptr, ntags, dptr, L):

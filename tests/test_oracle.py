@@ -67,3 +67,26 @@ def test_block_range_encode_is_a_slice(oracle):
 def test_test6_regenerates():
     assert hashlib.sha256(fixture_file("test6.txt")).hexdigest() == \
         "f07be2d96f37df76af247ea305452706f6558d17a01f04e6550dbfc89c8d7cdd"
+
+
+def test_cxx_prove_verifies_against_cxx_encode():
+    """The oracle's cxx prove / encode restatements agree with the cxx verify
+    equation (shacham_waters_private.cxx:791-842): sigma == sum v_i f(idx_i) +
+    sum alpha(j) mu_j mod p, sampled and check_all.  Parity unpinned."""
+    import hashlib
+    from oracle import oracle as O
+    p = int("db8709c32591ddc589b5c3c0986f92e0d11205b943c23a7e419e6c35b0256e6b", 16)
+    S = 4
+    data = b"".join(hashlib.sha256(b"o%d" % i).digest() for i in range(50)) + b"xyz"
+    fk, ak, ck = b"f" * 32, b"a" * 32, b"c" * 32
+    tags = O.cxx_encode(p, S, fk, ak, data)
+    n = len(tags)
+    for chunks in (5, n, n + 3):
+        mu, sigma = O.cxx_prove(p, S, ck, chunks, p, n, lambda k: tags[k],
+                                lambda off, m: data[off:off + m])
+        rhs = 0
+        for i in range(min(chunks, n) if chunks >= n else chunks):
+            idx = i if chunks >= n else O.cxx_prf_eval(ck, n, i)[0]
+            rhs += O.cxx_prf_eval(ck, p, i)[0] * O.cxx_prf_eval(fk, p, idx)[0]
+        rhs += sum(O.cxx_prf_eval(ak, p, j)[0] * mu[j] for j in range(S))
+        assert sigma == rhs % p, chunks
