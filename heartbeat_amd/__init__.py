@@ -5,9 +5,10 @@ encode/prove hot path behind the heartbeat API.
     from heartbeat_amd import HeartbeatError
 
 Compute runs in hand-written HIP kernels for gfx950 (libhbswizzle.so, C ABI in
-include/hbswizzle.h); see DESIGN.md.  The C++ ``heartbeat.Swizzle`` object and
-the Merkle / OneHash schemes are outside this build's scope, so
-``Heartbeat`` is the PySwizzle scheme here.
+include/hbswizzle.h); see DESIGN.md.  ``heartbeat_amd.Swizzle.Swizzle`` mirrors
+the C++ extension's ``heartbeat.Swizzle`` object over the kernels' cxx mode
+(parity unpinned).  The Merkle / OneHash schemes are outside this build's
+scope, so ``Heartbeat`` is the PySwizzle scheme here.
 """
 __version__ = "0.1.4"
 
