@@ -1,34 +1,52 @@
 #!/usr/bin/env python3
 """Swizzle encode benchmark (BASELINE.json metric: GiB/s of file bytes tagged,
-Swizzle encode, device-resident).
+Swizzle encode, device-resident, at 1/2/4/8 GPUs).
 
 One step = one pass of the encode hot path (hb_encode: alpha PRF + Montgomery
-conversion + the encode kernel) over every block of this rank's device-resident
-synthetic file.  Workload (BASELINE.json configs):
+conversion + prefix image + the encode kernels) over every block of this
+rank's device-resident synthetic file.  Workloads (BASELINE.json configs):
   c3 (default): configs[2], 64 GiB random file, 256-bit prime, 16 sectors per
                 block -- the largest single-GPU configuration; for N > 1 every
-                rank encodes its own 64 GiB block-range shard of an N*64 GiB file
-                (weak scaling, no collective: blocks are independent).
+                rank encodes its own 64 GiB block-range shard of an N*64 GiB
+                file (weak scaling, no collective: blocks are independent).
   c2:           configs[1], 1 GiB, 256-bit prime, 1 sector per block.
-  c4:           configs[3], 256 GiB file sharded over the N ranks (256/N GiB each).
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run, one rank per GPU (RCCL is used only for the barrier and
-the max-over-ranks time).
+  c4:           configs[3], ONE 256 GiB file sharded over the N ranks (strong
+                scaling, 256/N GiB per rank).  A rank whose share does not fit
+                in HBM next to its tags (N = 1) holds it as consecutive
+                resident pieces; only the encode calls are timed.
+  c5:           configs[4], prove() on a 64 GiB device-resident file with a
+                10,000-index challenge (ms per proof).
+
+Launch: `python bench.py [--gpus N --steps K --warmup W]`.  With N > 1 and no
+torch.distributed environment the script starts N ranks itself (one process
+per GPU, LOCAL_RANK = GPU ordinal) before touching any GPU; under
+`torch.distributed.run` it is one of the launched ranks.  Ranks share nothing
+but a gloo barrier and the max-over-ranks time (no data-path collective; the
+control plane does not need RCCL).
 
 Besides the contract fields the JSON line carries
-  roofline:     the encode kernel's algorithmic file bytes per launch / its mean
-                duration (HIP events on the kernel's stream) against the HBM
-                read peak; traffic from the rocprofv3 PMC pass when recorded in
-                profiles/ for this workload, else null; plus the LDS-lookup
-                rate, the resource that actually binds.
-  cpu_baseline: the repo's C oracle (OpenSSL AES-NI + BIGNUM, pthreads) timed on
-                this host on a bounded prefix of the same file (rank 0, N = 1).
+  roofline:     the encode kernels' algorithmic file bytes per launch / their
+                mean duration (HIP events on the kernel stream) against the HBM
+                read peak (vendor 8.0 TB/s; `peak_measured` = hb_stream_read on
+                the same buffer), traffic from the committed rocprofv3 PMC pass
+                when it matches this workload, and the LDS-lookup and VALU
+                resources that actually bind;
+  parity_sample: >= 10,000 random blocks plus the first and last 1,000 (the
+                tail block included) of every rank's tags, after the timed
+                region, against the CPU oracle;
+  cpu_baseline: the repo's C oracle (OpenSSL AES-NI + BIGNUM, pthreads) on a
+                bounded prefix of the same file, and the pure-Python PySwizzle
+                restatement (oracle/pyswizzle_port.py) on 1 MiB and on a
+                bounded prefix of 64 MiB, single core (rank 0, N = 1).
 """
 import argparse
 import ctypes
 import hashlib
 import json
 import os
+import platform
+import random
+import subprocess
 import sys
 import time
 
@@ -41,6 +59,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E vendor peak (MI355X_MICROARCH.md)
 LDS_LOOKUPS_PER_CLK_CU = 32.0  # one wave-wide ds_read_b32 per 2 clocks per CU
 CLOCK_GHZ = 2.4
 NUM_CUS = 256
+MAX_RESIDENT_GIB = 160         # per-rank resident file bytes (HBM 288 GB minus tags / scratch)
+METRIC = "GiB/s file bytes tagged (Swizzle encode, device-resident) at 1/2/4/8 GPUs"
 
 CONFIGS = {
     "c3": dict(name="configs[2]: 64 GiB random file, Swizzle encode, 256-bit prime, "
@@ -53,12 +73,12 @@ CONFIGS = {
                     "challenge, 256-bit prime, 16 sectors/block, 1 MI355X",
                gib_per_rank=64, sectors=16, weak=True, prove_chunks=10000),
     "c4": dict(name="configs[3]: 256 GiB random file, Swizzle encode, 256-bit prime, "
-                    "16 sectors/block, block ranges sharded over N GPUs",
+                    "16 sectors/block, block ranges sharded over N GPUs (no collective)",
                gib_total=256, sectors=16, weak=False),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -66,8 +86,13 @@ def parse():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--gib", type=float, default=None, help="override file GiB per rank")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="oracle threads (default: this process's CPU share, $OMP_NUM_THREADS or affinity)")
+    ap.add_argument("--py-seconds", type=float, default=15.0,
+                    help="budget of the pure-Python PySwizzle row on the 64 MiB input")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity-sample", action="store_true")
+    ap.add_argument("--parity-blocks", type=int, default=10000)
     ap.add_argument("--single-pass", action="store_true",
                     help="one-pass PRF engine instead of prefix-image first pass + retry pass")
     ap.add_argument("--prf", default="pyswizzle", choices=["pyswizzle", "cxx"],
@@ -75,120 +100,249 @@ def parse():
                          "cxx Swizzle extension's PRF (cxx/prf.hxx, CFB-128), parity unpinned")
     ap.add_argument("--host-path", action="store_true",
                     help="also time the pinned/pageable host path on a 4 GiB prefix (DESIGN.md)")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="exercise the launch / rank / timing / JSON plumbing without HIP calls (CPU tests)")
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
+# ---------------------------------------------------------------- ranks
+def spawn_ranks(args):
+    """Start args.gpus ranks of this script (one process per GPU) and return
+    the worst exit code.  Runs before anything touches a GPU."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(args.gpus),
+                    "LOCAL_WORLD_SIZE": str(args.gpus), "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(port)})
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        p.wait()
+        rc = rc or p.returncode
+    return rc
+
+
+class Ranks(object):
+    """This process's place in the job and the gloo control plane."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def reduce(self, x, op):
+        """x (float) reduced over ranks with op in {"max", "min", "sum"}."""
+        if self.dist is None:
+            return x
         import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        o = {"max": self.dist.ReduceOp.MAX, "min": self.dist.ReduceOp.MIN,
+             "sum": self.dist.ReduceOp.SUM}[op]
+        self.dist.all_reduce(t, op=o)
+        return float(t.item())
 
-    from heartbeat_amd import _native
-    L = _native.lib()
-    ctx = _native.context(local)
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
 
-    cfg = CONFIGS[args.config]
+
+# ---------------------------------------------------------------- workload
+def plan_for(args, cfg, world, rank):
+    from heartbeat_amd.shard import shard_plan
     S = cfg["sectors"]
-    p = P256
-    pb = _native.be(p)
-    ss, w = 32, 32
-    C = ss * S
+    C = 32 * S
     if args.gib is not None:
         file_len = int(args.gib * GIB) * world
     elif cfg["weak"]:
         file_len = cfg["gib_per_rank"] * GIB * world
     else:
         file_len = cfg["gib_total"] * GIB
-    # rank r encodes its block range of one file of file_len bytes
-    from heartbeat_amd.shard import shard_plan
     plan = shard_plan(file_len, C, rank, world)
-    global_blocks = plan["total_blocks"]
+    # resident pieces of this rank's share (whole blocks)
+    max_piece = MAX_RESIDENT_GIB * GIB // C * C
+    pieces = []
+    off = 0
+    while True:
+        n = min(max_piece, plan["byte_len"] - off)
+        pieces.append((off, n))
+        off += n
+        if off >= plan["byte_len"]:
+            break
+    return file_len, plan, pieces
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    R = Ranks()
+    try:
+        if args.dry_run:
+            return dry_run(args, R)
+        cfg = CONFIGS[args.config]
+        if "prove_chunks" in cfg:
+            return bench_prove(args, cfg, R)
+        return bench_encode(args, cfg, R)
+    finally:
+        R.close()
+
+
+def dry_run(args, R):
+    """The launch / barrier / max-over-ranks / JSON path with a sleep for a step."""
+    cfg = CONFIGS[args.config]
+    file_len, plan, pieces = plan_for(args, cfg, R.world, R.rank)
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    R.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.002 * (1 + R.rank))
+    R.barrier()
+    elapsed = R.reduce(time.perf_counter() - t0, "max")
+    blocks = R.reduce(plan["nblocks"], "sum")
+    if R.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": R.world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak" if cfg["weak"] else "strong", "dry_run": True,
+                          "config": {"workload": cfg["name"], "file_bytes": file_len,
+                                     "blocks_total": plan["total_blocks"], "blocks_summed": int(blocks),
+                                     "pieces_rank0": len(pieces)}}), flush=True)
+
+
+def bench_encode(args, cfg, R):
+    from heartbeat_amd import _native
+    L = _native.lib()
+    ctx = _native.context(R.local)
+    S = cfg["sectors"]
+    p = P256
+    pb = _native.be(p)
+    w = 32
+    C = 32 * S
+    file_len, plan, pieces = plan_for(args, cfg, R.world, R.rank)
     b0 = plan["b0"]
     nblocks = plan["nblocks"]
-    length = plan["byte_len"]                        # this rank's bytes
-
+    length = plan["byte_len"]
     fk = hashlib.sha256(b"hb-bench-f").digest()
     ak = hashlib.sha256(b"hb-bench-alpha").digest()
+    seed = 0x5EED0000 + 3 + R.rank
 
+    piece_bytes = max(n for _, n in pieces)
     dptr = ctypes.c_void_p()
     tptr = ctypes.c_void_p()
-    ctx.check(L.hb_device_malloc(ctx.h, length, ctypes.byref(dptr)))
+    ctx.check(L.hb_device_malloc(ctx.h, max(piece_bytes, 16), ctypes.byref(dptr)))
     ctx.check(L.hb_device_malloc(ctx.h, nblocks * w, ctypes.byref(tptr)))
-    # each rank fills its shard from its own seeded stream (bytes do not affect the work)
-    ctx.check(L.hb_fill_random(ctx.h, dptr, length, 0x5EED0000 + 3 + rank))
-    if "prove_chunks" in cfg:
-        return bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak, C, rank)
 
+    def fill(k):
+        # resident piece k of this rank's share, its own seeded stream
+        ctx.check(L.hb_fill_random(ctx.h, dptr, pieces[k][1], seed ^ (k << 24)))
+
+    fill(0)
     tries = ctypes.c_uint64()
     cxx = args.prf == "cxx"
     flags = 3 | (_native.HB_ENCODE_SINGLE_PASS if args.single_pass else 0) | (_native.HB_PRF_CXX if cxx else 0)
+    tries_total = [0]
 
-    def step():
-        ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, b0, dptr, length, nblocks, tptr,
-                              flags, ctypes.byref(tries)))
+    def encode_piece(k):
+        off, n = pieces[k]
+        pb0 = off // C                                   # first block of the piece in the rank
+        last = k == len(pieces) - 1
+        nb = (nblocks - pb0) if last else n // C
+        ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, b0 + pb0, dptr, n, nb,
+                              tptr.value + pb0 * w, flags, ctypes.byref(tries)))
+        tries_total[0] += tries.value
         return ctx.last_kernel_ms()[0]
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+    def step():
+        """Encode this rank's whole share; returns (wall s, kernel ms) of the
+        encode calls only (piece refills, when there are several, excluded)."""
+        wall, kms = 0.0, 0.0
+        for k in range(len(pieces)):
+            if len(pieces) > 1:
+                fill(k)
+            t = time.perf_counter()
+            kms += encode_piece(k)
+            wall += time.perf_counter() - t
+        return wall, kms
 
     for _ in range(args.warmup):
         step()
-    barrier()
+    tries_total[0] = 0
+    R.barrier()
     t0 = time.perf_counter()
-    kms = []
+    kms_list = []
+    wall_sum = 0.0
     for _ in range(args.steps):
-        kms.append(step())
-    barrier()
+        wall, kms = step()
+        wall_sum += wall
+        kms_list.append(kms)
+    R.barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if len(pieces) > 1:
+        elapsed = wall_sum          # refills of the resident piece are not part of the encode
+    elapsed = R.reduce(elapsed, "max")
 
     total_bytes = file_len * args.steps
     value = total_bytes / GIB / elapsed
-    kernel_ms = sum(kms) / len(kms)
+    kernel_ms = sum(kms_list) / len(kms_list)
     achieved_gbs = length / (kernel_ms * 1e-3) / 1e9
-    tries_per_block = tries.value / nblocks
-    # nb = 32 byte-0 AES-256 per try (197 LDS lookups each); the two-pass
-    # encode replaces the first 4 of every block's first try by prefix-image
-    # loads and builds that image (2^24 + 2^16 + 2^8 AES) once per step
+    tries_total = tries_total[0] / args.steps
+    tries_per_block = tries_total / nblocks
     if cxx:
-        # cxx prf: 2 full AES-256 per try (CFB-128 over 32 bytes), 16 * 14 lookups each
-        aes = tries.value * 2
+        aes = tries_total * 2                      # CFB-128 over 32 bytes: 2 full AES per try
         lookups = aes * 16 * 14
     else:
-        aes = tries.value * 32
+        aes = tries_total * 32                     # nb = 32 byte-0 AES per try
         if not args.single_pass:
-            aes += (1 << 24) + (1 << 16) + (1 << 8) - 4 * nblocks
+            # the first 4 of every block's first try come from the prefix image,
+            # built once per step (2^24 + 2^16 + 2^8 byte-0 AES) per piece
+            aes += len(pieces) * ((1 << 24) + (1 << 16) + (1 << 8)) - 4 * nblocks
         lookups = aes * (16 * 12 + 5)
     lds_rate = lookups / (kernel_ms * 1e-3)
     lds_peak = NUM_CUS * CLOCK_GHZ * 1e9 * LDS_LOOKUPS_PER_CLK_CU
 
     traffic = None
+    pmc = None
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
             rec = json.load(open(prof)).get(args.config + ("_cxx" if cxx else ""))
-            if rec and rec.get("file_bytes") == length:
+            if rec and rec.get("file_bytes") == length and len(pieces) == 1:
                 traffic = rec["hbm_bytes_per_launch"]
+                pmc = {k: rec[k] for k in ("valu_busy", "lds_busy", "source_valu") if k in rec} or None
         except (ValueError, KeyError):
             traffic = None
 
+    # measured streaming-read peak on the same buffer (outside the timed region)
+    peak_measured = None
+    ms = ctypes.c_double()
+    nread = piece_bytes // 16 * 16
+    if nread:
+        for _ in range(2):          # the second pass is the measurement
+            ctx.check(L.hb_stream_read(ctx.h, dptr, nread, ctypes.byref(ms)))
+        peak_measured = round(nread / (ms.value * 1e-3) / 1e9, 1)
+
     line = {
-        "metric": "GiB/s file bytes tagged (Swizzle encode, device-resident) at 1/2/4/8 GPUs",
+        "metric": METRIC,
         "value": round(value, 3),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": R.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -201,125 +355,136 @@ def main():
             "workload": cfg["name"],
             "file_bytes": file_len,
             "file_bytes_per_rank": length,
-            "blocks_total": global_blocks,
+            "resident_pieces_per_rank": len(pieces),
+            "blocks_total": plan["total_blocks"],
             "sectors": S,
             "prime_bits": 256,
             "prime": hex(p),
             "expected_tries_per_prf": round(2.0 ** 256 / p, 4),
             "prf": "cxx Swizzle prf (cxx/prf.hxx:125-176, CFB-128 over SHA256(LE32 i)); parity unpinned"
                    if cxx else "PySwizzle KeyedPRF (util.py:83-96, CFB-8 over SHA256(str(i))); bit-exact",
-            "parallelism": "dp%d block-range shards, no collective" % world,
+            "parallelism": "dp%d block-range shards, no collective (gloo barrier + max time only)" % R.world,
         },
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved_gbs, 1),
             "peak": HBM_PEAK_GBS,
+            "peak_measured": peak_measured,
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "frac_of_measured": round(achieved_gbs / peak_measured, 4) if peak_measured else None,
             "traffic": traffic,
             "kernel": "hb_cxx_encode_kernel" if cxx else "hb_encode_kernel" if args.single_pass else
                       "hb_prefix_kernel + hb_encode_first_kernel + hb_encode_retry_kernel",
             "kernel_ms": round(kernel_ms, 3),
             "algorithmic_bytes_per_launch": length,
             "binding_resource": {
-                "resource": "LDS ds_read_b32 T-table lookups",
+                "resource": "LDS ds_read_b32 T-table lookups (VALU issue co-binding, DESIGN.md 5.1)",
                 "achieved_per_s": lds_rate,
                 "peak_per_s": lds_peak,
                 "frac": round(lds_rate / lds_peak, 4),
+                "pmc": pmc,
             },
         },
         "prf_tries_per_block": round(tries_per_block, 4),
         "aes_per_block": round(aes / nblocks, 3),
     }
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C,
-                                            args.cpu_seconds, args.cpu_threads, cxx)
-    if rank == 0 and args.host_path:
-        line["host_path"] = host_path(ctx, L, dptr, length, S, pb, fk, ak, C)
+    if not args.no_parity_sample:
+        ok, n = parity_sample(ctx, L, dptr, tptr, pieces, plan, S, p, fk, ak, C, w, args, cxx, fill)
+        n_all = int(R.reduce(n, "sum"))
+        ok_all = R.reduce(1.0 if ok else 0.0, "min") == 1.0
+        line["parity_sample"] = {"n": n_all, "ok": ok_all,
+                                 "what": ">= %d random blocks + first/last 1,000 per rank (tail included) "
+                                         "vs oracle/swizzle_oracle.c" % args.parity_blocks}
+    if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
+        if len(pieces) > 1:
+            fill(0)
+        line["cpu_baseline"] = cpu_baseline(ctx, L, dptr, pieces[0][1], S, p, fk, ak, C,
+                                            args.cpu_seconds, args.cpu_threads, args.py_seconds, cxx)
+    if R.rank == 0 and args.host_path:
+        line["host_path"] = host_path(ctx, L, dptr, pieces[0][1], S, pb, fk, ak, C)
 
-    if rank == 0:
+    if R.rank == 0:
         print(json.dumps(line), flush=True)
     ctx.check(L.hb_device_free(ctx.h, dptr))
     ctx.check(L.hb_device_free(ctx.h, tptr))
-    if dist is not None:
-        dist.destroy_process_group()
 
 
-def bench_prove(args, cfg, ctx, L, dptr, tptr, length, nblocks, S, p, pb, fk, ak, C, rank):
-    """configs[4]: one step = one PySwizzle.prove (PySwizzle.py:333-370) over
-    the device-resident file and tags: idx / v PRFs for `chunks` indices, the
-    gathered weighted sums of the S sector columns and of the tags, and the
-    mod-p reductions, with mu and sigma copied back to the host."""
-    chunks = cfg["prove_chunks"]
-    # --prf cxx: the cxx extension's prove (shacham_waters_private.cxx:731-789)
-    from heartbeat_amd import _native
-    cxx = args.prf == "cxx"
-    pflags = 3 | (_native.HB_PRF_CXX if cxx else 0)
-    ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, dptr, length, nblocks, tptr, pflags, None))
-    ck = hashlib.sha256(b"hb-bench-challenge").digest()
-    vb = pb                                   # v_max = p, as gen_challenge (PySwizzle.py:329)
-    w = 32
-    mu = ctypes.create_string_buffer(w * S)
-    sg = ctypes.create_string_buffer(w)
-
-    def step():
-        ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, ck, len(ck), chunks, vb, len(vb), tptr, nblocks,
-                             dptr, length, pflags, mu, sg))
-
-    for _ in range(max(1, args.warmup)):
-        step()
-    steps = max(args.steps, 20)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    ms = (time.perf_counter() - t0) / steps * 1e3
-    line = {
-        "metric": "Swizzle prove() latency, ms per proof (device-resident file and tags)",
-        "value": round(ms, 4), "unit": "ms", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
-        "ms_per_step": round(ms, 4), "higher_is_better": False, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic (SplitMix64 random file bytes, seeded keys)",
-        "config": {"workload": cfg["name"], "file_bytes": length, "blocks_total": nblocks,
-                   "sectors": S, "prime_bits": 256, "chunks": chunks,
-                   "prf": "cxx prf, cxx prove (parity unpinned)" if cxx else "PySwizzle KeyedPRF"},
-        "gathered_bytes_per_proof": chunks * (C + w),
-    }
-    if rank == 0 and not args.no_cpu_baseline and not cxx:
-        import numpy as np
-        from oracle import oracle as O
-        host = np.empty(length, dtype=np.uint8)
-        ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value, length, 2))
-        tags = np.empty(nblocks * w, dtype=np.uint8)
-        ctx.check(L.hb_memcpy(ctx.h, tags.ctypes.data, tptr.value, nblocks * w, 2))
-        t = time.perf_counter()
-        n = 0
-        while n < 3 or time.perf_counter() - t < min(args.cpu_seconds, 5.0):
-            ref_mu = ctypes.create_string_buffer(w * S)
-            ref_sg = ctypes.create_string_buffer(w)
-            rc = O.lib().hbo_prove(pb, len(pb), S, ck, len(ck), chunks, vb, len(vb), nblocks,
-                                   ctypes.cast(tags.ctypes.data, ctypes.c_char_p), w,
-                                   host.ctypes.data, length, ref_mu, ref_sg)
-            if rc:
-                raise RuntimeError("oracle prove error %d" % rc)
-            n += 1
-        cpu_ms = (time.perf_counter() - t) / n * 1e3
-        line["cpu_baseline"] = {"value": round(cpu_ms, 3), "unit": "ms", "cores": 1, "kind": "port",
-                                "sample": "%d proofs of the same challenge, oracle/swizzle_oracle.c "
-                                          "(OpenSSL), 1 thread" % n}
-        line["proof_equal_oracle"] = ref_mu.raw == mu.raw and ref_sg.raw == sg.raw
-        del host, tags
-    print(json.dumps(line), flush=True)
-    ctx.check(L.hb_device_free(ctx.h, dptr))
-    ctx.check(L.hb_device_free(ctx.h, tptr))
-
-
-def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads, cxx=False):
-    """Oracle (kind "port") on successive 256 MiB prefixes of the same file
-    until `seconds` of CPU work, on `threads` host threads."""
+def parity_sample(ctx, L, dptr, tptr, pieces, plan, S, p, fk, ak, C, w, args, cxx, fill):
+    """After the timed region: this rank's first and last 1,000 blocks (the
+    last rank's include the PRF-only tail block) and >= parity_blocks random
+    blocks, GPU tags vs the oracle.  Returns (all equal, blocks checked)."""
     import numpy as np
     from oracle import oracle as O
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    nblocks = plan["nblocks"]
+    rng = random.Random(0x5A11 + plan["b0"])
+    picks = set(range(min(1000, nblocks))) | set(range(max(0, nblocks - 1000), nblocks))
+    while len(picks) < min(nblocks, args.parity_blocks + 2000):
+        picks.add(rng.randrange(nblocks))
+    picks = sorted(picks)
+    tags = np.empty(nblocks * w, dtype=np.uint8)
+    ctx.check(L.hb_memcpy(ctx.h, tags.ctypes.data, tptr.value, nblocks * w, 2))
+    enc = O.cxx_encode if cxx else O.encode
+    ok = True
+    k = 0
+    # walk the pieces (refill when there are several: the buffer holds the last one)
+    for pi, (off, n) in enumerate(pieces):
+        if len(pieces) > 1:
+            fill(pi)
+        pb0, pb1 = off // C, (nblocks if pi == len(pieces) - 1 else (off + n) // C)
+        sel = [b for b in picks if pb0 <= b < pb1]
+        # contiguous runs: one copy and one oracle call each
+        i = 0
+        while i < len(sel):
+            j = i
+            while j + 1 < len(sel) and sel[j + 1] == sel[j] + 1:
+                j += 1
+            r0, r1 = sel[i], sel[j] + 1
+            lo = (r0 - pb0) * C
+            hi = min((r1 - pb0) * C, n)
+            data = np.empty(max(hi - lo, 0), dtype=np.uint8)
+            if hi > lo:
+                ctx.check(L.hb_memcpy(ctx.h, data.ctypes.data, dptr.value + lo, hi - lo, 2))
+            want = enc(p, S, fk, ak, data, block_base=plan["b0"] + r0, nblocks=r1 - r0, nthreads=4)
+            got = tags[r0 * w:r1 * w].tobytes()
+            ok = ok and got == b"".join(t.to_bytes(w, "big") for t in want)
+            k += r1 - r0
+            i = j + 1
+    return ok, k
+
+
+def host_cpu_info():
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name:"):
+                info["lscpu_model"] = ln.split(":", 1)[1].strip()
+    except Exception:
+        info["lscpu_model"] = platform.processor() or None
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    return info
+
+
+def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads, py_seconds, cxx=False):
+    """Oracle (kind "port") on successive 256 MiB prefixes of the same file
+    until `seconds` of CPU work, on this process's CPU share; plus the
+    single-core pure-Python PySwizzle restatement on 1 MiB and a bounded
+    prefix of a 64 MiB input."""
+    import io
+    import numpy as np
+    from oracle import oracle as O
+    info = host_cpu_info()
+    if threads is None:
+        # the GPU box gives each GPU a 16-core share and exports it as
+        # OMP_NUM_THREADS; nproc there counts the whole machine
+        threads = int(os.environ.get("OMP_NUM_THREADS") or info.get("affinity") or os.cpu_count() or 1)
+    threads = max(1, threads)
     piece = (256 << 20) // C * C
     host = np.empty(piece, dtype=np.uint8)
     out = np.empty((piece // C) * 32, dtype=np.uint8)
@@ -337,13 +502,46 @@ def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads, cxx=Fa
             raise RuntimeError("oracle error %d" % rc)
         done += n
         off += n
-    return {"value": round(done / GIB / busy, 4), "unit": "GiB/s", "cores": threads,
-            "kind": "port",
-            "sample": "%d MiB prefix of the same synthetic file (%d blocks), oracle/swizzle_oracle.c "
-                      "(%s), %d pthreads, %.1f s" % (
-                          done >> 20, done // C,
-                          "cxx prf: OpenSSL AES-NI CFB-128 + BIGNUM" if cxx else
-                          "OpenSSL AES-NI CFB8 + BIGNUM", threads, busy)}
+    res = {"value": round(done / GIB / busy, 4), "unit": "GiB/s", "cores": threads,
+           "kind": "port",
+           "sample": "%d MiB prefix of the same synthetic file (%d blocks), oracle/swizzle_oracle.c "
+                     "(%s), %d pthreads, %.1f s" % (
+                         done >> 20, done // C,
+                         "cxx prf: OpenSSL AES-NI CFB-128 + BIGNUM" if cxx else
+                         "OpenSSL AES-NI CFB8 + BIGNUM", threads, busy),
+           "host": info}
+    if cxx:
+        return res
+    # the "PySwizzle" row: pure Python, one core, the reference's algorithmic cost
+    from oracle import pyswizzle_port as PP
+    rows = []
+    ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value, min(64 << 20, length, piece), 2))
+    for label, size, budget in (("1 MiB input", 1 << 20, None), ("64 MiB input", 64 << 20, py_seconds)):
+        size = min(size, length, piece)
+        src = io.BytesIO(host[:size].tobytes())
+        t = time.perf_counter()
+        if budget is None:
+            PP.encode(p, S, fk, ak, src)
+            nbytes = size
+        else:
+            # whole blocks until the budget is spent (rate over the processed prefix)
+            f = PP.KeyedPRF(fk, p)
+            a = PP.KeyedPRF(ak, p)
+            nbytes = 0
+            blk = 0
+            while nbytes + C <= size and time.perf_counter() - t < budget:
+                sigma = f.eval(blk)
+                for j in range(S):
+                    buf = src.read(32)
+                    sigma += a.eval(j) * int.from_bytes(buf, "big")
+                sigma %= p
+                nbytes += C
+                blk += 1
+        dt = time.perf_counter() - t
+        rows.append({"value": round(nbytes / (1 << 20) / dt, 3), "unit": "MiB/s", "cores": 1,
+                     "kind": "port", "sample": "%s: %.2f MiB encoded in %.1f s" % (label, nbytes / (1 << 20), dt)})
+    res["pyswizzle_rows"] = rows
+    return res
 
 
 def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
@@ -381,6 +579,91 @@ def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
     out["pinned_tags_equal_pageable"] = ok
     out["unit"] = "GiB/s"
     return out
+
+
+def bench_prove(args, cfg, R):
+    """configs[4]: one step = one PySwizzle.prove (PySwizzle.py:333-370) over
+    the device-resident file and tags: idx / v PRFs for `chunks` indices, the
+    gathered weighted sums of the S sector columns and of the tags, and the
+    mod-p reductions, with mu and sigma copied back to the host."""
+    from heartbeat_amd import _native
+    L = _native.lib()
+    ctx = _native.context(R.local)
+    S = cfg["sectors"]
+    p = P256
+    pb = _native.be(p)
+    C = 32 * S
+    w = 32
+    length = int(args.gib * GIB) if args.gib is not None else cfg["gib_per_rank"] * GIB
+    nblocks = length // C + 1
+    fk = hashlib.sha256(b"hb-bench-f").digest()
+    ak = hashlib.sha256(b"hb-bench-alpha").digest()
+    dptr = ctypes.c_void_p()
+    tptr = ctypes.c_void_p()
+    ctx.check(L.hb_device_malloc(ctx.h, length, ctypes.byref(dptr)))
+    ctx.check(L.hb_device_malloc(ctx.h, nblocks * w, ctypes.byref(tptr)))
+    ctx.check(L.hb_fill_random(ctx.h, dptr, length, 0x5EED0000 + 3 + R.rank))
+    chunks = cfg["prove_chunks"]
+    cxx = args.prf == "cxx"
+    pflags = 3 | (_native.HB_PRF_CXX if cxx else 0)
+    ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, dptr, length, nblocks, tptr, pflags, None))
+    ck = hashlib.sha256(b"hb-bench-challenge").digest()
+    vb = pb                                   # v_max = p, as gen_challenge (PySwizzle.py:329)
+    mu = ctypes.create_string_buffer(w * S)
+    sg = ctypes.create_string_buffer(w)
+
+    def step():
+        ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, ck, len(ck), chunks, vb, len(vb), tptr, nblocks,
+                             dptr, length, pflags, mu, sg))
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    steps = max(args.steps, 20)
+    R.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    R.barrier()
+    ms = R.reduce((time.perf_counter() - t0) / steps * 1e3, "max")
+    line = {
+        "metric": "Swizzle prove() latency, ms per proof (device-resident file and tags)",
+        "value": round(ms, 4), "unit": "ms", "n_gpus": R.world, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": False, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (SplitMix64 random file bytes, seeded keys)",
+        "config": {"workload": cfg["name"], "file_bytes": length, "blocks_total": nblocks,
+                   "sectors": S, "prime_bits": 256, "chunks": chunks,
+                   "prf": "cxx prf, cxx prove (parity unpinned)" if cxx else "PySwizzle KeyedPRF"},
+        "gathered_bytes_per_proof": chunks * (C + w),
+    }
+    if R.rank == 0 and not args.no_cpu_baseline and not cxx:
+        import numpy as np
+        from oracle import oracle as O
+        host = np.empty(length, dtype=np.uint8)
+        ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value, length, 2))
+        tags = np.empty(nblocks * w, dtype=np.uint8)
+        ctx.check(L.hb_memcpy(ctx.h, tags.ctypes.data, tptr.value, nblocks * w, 2))
+        t = time.perf_counter()
+        n = 0
+        while n < 3 or time.perf_counter() - t < min(args.cpu_seconds, 5.0):
+            ref_mu = ctypes.create_string_buffer(w * S)
+            ref_sg = ctypes.create_string_buffer(w)
+            rc = O.lib().hbo_prove(pb, len(pb), S, ck, len(ck), chunks, vb, len(vb), nblocks,
+                                   ctypes.cast(tags.ctypes.data, ctypes.c_char_p), w,
+                                   host.ctypes.data, length, ref_mu, ref_sg)
+            if rc:
+                raise RuntimeError("oracle prove error %d" % rc)
+            n += 1
+        cpu_ms = (time.perf_counter() - t) / n * 1e3
+        line["cpu_baseline"] = {"value": round(cpu_ms, 3), "unit": "ms", "cores": 1, "kind": "port",
+                                "sample": "%d proofs of the same challenge, oracle/swizzle_oracle.c "
+                                          "(OpenSSL), 1 thread" % n}
+        line["proof_equal_oracle"] = ref_mu.raw == mu.raw and ref_sg.raw == sg.raw
+        del host, tags
+    if R.rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.check(L.hb_device_free(ctx.h, dptr))
+    ctx.check(L.hb_device_free(ctx.h, tptr))
 
 
 if __name__ == "__main__":

@@ -300,7 +300,9 @@ class PySwizzle(object):
         tags_raw = tag.raw(p)
         key = _kb(chal.key)
         vmax = _native.be(int(chal.v_max))
-        fb = FileBuffer(file)
+        # absolute offsets from the start of the file, as the reference's
+        # file.seek(pos) before every read (PySwizzle.py:353-355)
+        fb = FileBuffer(file, from_start=True)
         try:
             mu = ctypes.create_string_buffer(w * S)
             sg = ctypes.create_string_buffer(w)
@@ -312,6 +314,7 @@ class PySwizzle(object):
                                                  vmax, len(vmax), tarr.ctypes.data, ntags,
                                                  fb.addr, fb.len, 0, mu, sg))
         finally:
+            fb.restore()
             fb.close()
         proof.mu = [int.from_bytes(mu.raw[j * w:(j + 1) * w], "big") for j in range(S)]
         proof.sigma = int.from_bytes(sg.raw, "big")

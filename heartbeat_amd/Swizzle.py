@@ -135,7 +135,9 @@ class Swizzle(object):
         tarr = np.frombuffer(tag.raw(p), dtype=np.uint8)
         key = _kb(chal.key)
         vmax = _native.be(int(chal.v_max))
-        fb = FileBuffer(file)
+        # absolute offsets from the start of the file, as the reference's
+        # file.seek(pos) before every read (PySwizzle.py:353-355)
+        fb = FileBuffer(file, from_start=True)
         try:
             mu = ctypes.create_string_buffer(w * S)
             sg = ctypes.create_string_buffer(w)
@@ -146,6 +148,7 @@ class Swizzle(object):
                                                  len(vmax), tarr.ctypes.data, ntags, fb.addr, fb.len,
                                                  _native.HB_PRF_CXX, mu, sg))
         finally:
+            fb.restore()
             fb.close()
         proof.mu = [int.from_bytes(mu.raw[j * w:(j + 1) * w], "big") for j in range(S)]
         proof.sigma = int.from_bytes(sg.raw, "big")

@@ -1,8 +1,24 @@
 """Turn the reference's duck-typed file objects (read/seek/tell,
 README.md:13) into one contiguous host buffer without copying when possible:
 BytesIO -> its buffer, real files -> a read-only mmap, anything else -> read().
-The buffer starts at the file's current position, as PySwizzle's reads do
-(PySwizzle.py:299)."""
+
+Two views, matching the two ways the reference touches the file:
+
+* encode (``from_start=False``): the buffer starts at the file's CURRENT
+  position, as PySwizzle.encode's sequential ``file.read(sectorsize)`` calls do
+  (PySwizzle.py:299; cxx PythonSeekableFile::read, PythonSeekableFile.hxx:47-54);
+  ``consume()`` then leaves the file at EOF like those reads.
+* prove (``from_start=True``): the buffer is the WHOLE file from offset 0,
+  because prove seeks ABSOLUTE offsets ``index*chunk_size + j*sectorsize``
+  before every read (PySwizzle.py:353-355; cxx shacham_waters_private.cxx:
+  762-764), whatever the position the caller left the file at.  ``restore()``
+  puts the caller's position back (the reference leaves the file wherever its
+  last read ended; callers must not rely on either).
+
+A read()-only object without ``seek`` cannot be rewound: it is read from its
+current position in both views (the reference's prove would fail on it with
+an AttributeError on ``seek``).
+"""
 import io
 import mmap
 import os
@@ -11,14 +27,17 @@ import numpy as np
 
 
 class FileBuffer(object):
-    def __init__(self, file):
+    def __init__(self, file, from_start=False):
         self._mm = None
         self.file = file
-        start = 0
+        self.from_start = from_start
+        pos = 0
         try:
-            start = file.tell()
+            pos = file.tell()
         except Exception:
-            start = 0
+            pos = 0
+        self.pos = pos                       # caller's position, for restore()
+        start = 0 if from_start else pos
         self.start = start
         arr = None
         if isinstance(file, io.BytesIO):
@@ -42,6 +61,11 @@ class FileBuffer(object):
                 except (OSError, ValueError):
                     arr = None
             if arr is None:
+                if from_start:
+                    try:
+                        file.seek(0)
+                    except Exception:
+                        pass
                 data = file.read()
                 if isinstance(data, str):
                     data = data.encode("latin-1")
@@ -61,6 +85,13 @@ class FileBuffer(object):
                 self.file.seek(self.start + self.len)
             except Exception:
                 pass
+
+    def restore(self):
+        """Put the caller's file position back."""
+        try:
+            self.file.seek(self.pos)
+        except Exception:
+            pass
 
     def close(self):
         self.arr = None

@@ -37,6 +37,7 @@ SIGNATURES = [
     ("hb_last_error", _c.c_char_p, [_P]),
     ("hb_width", _c.c_size_t, [_B, _c.c_size_t]),
     ("hb_prf_eval", _c.c_int, [_P, _B, _c.c_size_t, _B, _c.c_size_t, _P, _c.c_size_t, _P]),
+    ("hb_prf_eval_digests", _c.c_int, [_P, _B, _c.c_size_t, _B, _c.c_size_t, _B, _c.c_size_t, _P]),
     ("hb_encode", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _B, _c.c_size_t, _c.c_uint64,
                              _P, _c.c_uint64, _c.c_uint64, _P, _c.c_uint32,
                              _c.POINTER(_c.c_uint64)]),
@@ -58,6 +59,7 @@ SIGNATURES = [
     ("hb_host_register", _c.c_int, [_P, _P, _c.c_uint64]),
     ("hb_host_unregister", _c.c_int, [_P, _P]),
     ("hb_fill_random", _c.c_int, [_P, _P, _c.c_uint64, _c.c_uint64]),
+    ("hb_stream_read", _c.c_int, [_P, _P, _c.c_uint64, _c.POINTER(_c.c_double)]),
 ]
 
 

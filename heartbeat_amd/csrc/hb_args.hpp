@@ -60,6 +60,7 @@ template <int NL>
 struct PrfArgs {
     PrfParams<NL> prf;
     const u64 *xs;                // inputs (device) or nullptr: x = x0 + k
+    const u32 *digs;              // or SHA-256 digests of the inputs (8 big-endian words each)
     u64 x0;
     u64 n;
     u32 *out;                     // n * NL little-endian limbs

@@ -89,6 +89,7 @@ inline double inv_scaled(const Limbs &p) {
     for (int t = nl - 1; t >= 0; --t) {
         double s = 1.0;
         int e = t - (nl - 2);
+        if (e < -31) continue;   // dropped as on the device (HbScale)
         for (int i = 0; i < (e >= 0 ? e : -e); ++i) s *= 4294967296.0;
         pd += (double)p[t] * (e >= 0 ? s : 1.0 / s);
     }

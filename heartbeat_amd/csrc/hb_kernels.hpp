@@ -115,6 +115,18 @@ __device__ __forceinline__ void hb_prf_digest(u64 x, u32 dig[8]) {
     else hb_sha256_decimal(x, dig);
 }
 
+// The digest a job's PRF input hashes to: handlers with precomputed digests
+// (hb_prf_eval_digests) provide digest(); the others hash x_of(job).
+template <int MODE, class H>
+__device__ __forceinline__ auto hb_job_digest(const H &h, u64 job, u32 dig[8], int)
+    -> decltype(h.digest(job, dig), void()) {
+    if (!h.digest(job, dig)) hb_prf_digest<MODE>(h.x_of(job), dig);
+}
+template <int MODE, class H>
+__device__ __forceinline__ void hb_job_digest(const H &h, u64 job, u32 dig[8], long) {
+    hb_prf_digest<MODE>(h.x_of(job), dig);
+}
+
 template <int NL, int NR, class H, int MODE = 0>
 __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParams<NL> &P,
                                           u64 njobs, unsigned long long *queue) {
@@ -124,7 +136,7 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
     u32 dig[8], sr[4] = {0, 0, 0, 0}, out[NL];
     if (active) {
         h.init(job, sr);
-        hb_prf_digest<MODE>(h.x_of(job), dig);
+        hb_job_digest<MODE>(h, job, dig, 0);
     }
     u32 tries = 0, job_tries = 0, failed = 0;
     while (__ballot(active)) {
@@ -153,7 +165,7 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
                 job_tries = 0;
                 if (got) {
                     h.init(job, sr);   // fresh cipher per eval (util.py:88) or a resumed stream
-                    hb_prf_digest<MODE>(h.x_of(job), dig);
+                    hb_job_digest<MODE>(h, job, dig, 0);
                 }
             }
         }
@@ -366,6 +378,13 @@ template <int NL>
 struct PrfHandler {
     const PrfArgs<NL> &A;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.xs ? A.xs[job] : A.x0 + job; }
+    // SHA-256 digests supplied by the host (inputs outside [0, 2^64): the
+    // reference hashes str(x) of any int, util.py:91)
+    __device__ __forceinline__ bool digest(u64 job, u32 dig[8]) const {
+        if (!A.digs) return false;
+        for (int t = 0; t < 8; ++t) dig[t] = A.digs[job * 8 + t];
+        return true;
+    }
     __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
     __device__ __forceinline__ void accept(u64 job, const u32 v[NL]) const {
         u32 *o = A.out + job * NL;

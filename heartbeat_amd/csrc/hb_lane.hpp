@@ -622,20 +622,24 @@ struct HbPow2 {   // 2^(32 E), E >= 0, as a compile-time double
 template <>
 struct HbPow2<0> { static constexpr double v = 1.0; };
 
-// 2^(32 (T - (NL - 2))): limb T of a value scaled so that NL+1 limbs of up to
-// 1056 bits stay inside the double exponent range.
+// 2^(32 (T - (NL - 2))): limb T of a value scaled so that NL+1 limbs stay
+// inside the double exponent range.  Limbs more than 31 limbs below the top
+// (NL = 64 only) are dropped: they move the quotient estimate by < 2^-960
+// relative, and the estimate is corrected by exact subtractions anyway.
 template <int NL, int T>
 struct HbScale {
     static constexpr int E = T - (NL - 2);
-    static constexpr double v = E >= 0 ? HbPow2<(E >= 0 ? E : 0)>::v : 1.0 / HbPow2<(E < 0 ? -E : 0)>::v;
+    static constexpr double v = E >= 0 ? HbPow2<(E >= 0 ? E : 0)>::v
+                              : E < -31 ? 0.0 : 1.0 / HbPow2<(E < 0 && E >= -31 ? -E : 0)>::v;
 };
 
 // v (NL+1 limbs, v < 2^32 p) -> v mod p in out (NL limbs).
 template <int NL>
 HB_HD void hb_reduce_small(u32 v[NL + 1], const ModP<NL> &P, u32 out[NL]) {
-    double vd = 0.0, sc = HbScale<NL, 0>::v;
+    constexpr int T0 = NL - 2 - 31 > 0 ? NL - 2 - 31 : 0;   // lowest limb HbScale keeps
+    double vd = 0.0, sc = HbScale<NL, T0>::v;
     HB_UNROLL
-    for (int t = 0; t <= NL; ++t) {
+    for (int t = T0; t <= NL; ++t) {
         vd += (double)v[t] * sc;
         sc *= 4294967296.0;
     }

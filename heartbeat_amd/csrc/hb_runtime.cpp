@@ -30,6 +30,7 @@ template <int NL> hipError_t hb_launch_mont(const MontArgs<NL> &, hipStream_t);
 template <int NL> hipError_t hb_launch_wsum(const WsumArgs<NL> &, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_sum(const SumArgs<NL> &, int, hipStream_t);
 hipError_t hb_launch_fill(unsigned char *, u64, u64, hipStream_t);
+hipError_t hb_launch_read(const void *, u64, u32 *, int, hipStream_t);
 
 namespace {
 
@@ -93,6 +94,7 @@ int nl_for_bits(int bits) {
     if (bits <= 256) return 8;
     if (bits <= 512) return 16;
     if (bits <= 1024) return 32;
+    if (bits <= 2048) return 64;
     return 0;
 }
 
@@ -137,12 +139,14 @@ int check_key(hb_ctx *c, size_t key_len) {
 // results as NL-limb little-endian values in out (device).
 template <int NL>
 int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be, size_t range_len,
-            const u64 *xs_dev, u64 x0, u64 n, u32 *out_dev, int queue_slot, int mode = 0) {
+            const u64 *xs_dev, u64 x0, u64 n, u32 *out_dev, int queue_slot, int mode = 0,
+            const u32 *digs_dev = nullptr) {
     PrfArgs<NL> A;
     int nr = 0;
     if (!make_prf<NL>(key, key_len, range_be, range_len, A.prf, nr))
         return fail(c, HB_EINVAL, "invalid PRF key");
     A.xs = xs_dev;
+    A.digs = digs_dev;
     A.x0 = x0;
     A.n = n;
     A.out = out_dev;
@@ -186,12 +190,13 @@ struct PrimeInfo {
 int parse_prime(hb_ctx *c, const uint8_t *p_be, size_t p_len, PrimeInfo &pi) {
     if (!p_be || p_len == 0) return fail(c, HB_EINVAL, "prime is empty");
     pi.bits = bitlen_be(p_be, p_len);
-    if (pi.bits < 9) return fail(c, HB_EINVAL, "prime must be at least 2^8 (sector size >= 1 byte)");
+    // sectorsize = bitlen(p) // 8 >= 1 (PySwizzle.py:255); smaller primes make
+    // the reference's encode loop never terminate (read(0) is never short)
+    if (pi.bits < 8) return fail(c, HB_EINVAL, "prime must be at least 2^7 (sector size >= 1 byte)");
     if (!(p_be[p_len - 1] & 1)) return fail(c, HB_EINVAL, "prime must be odd");
     pi.nl = nl_for_bits(pi.bits);
     if (pi.nl < 8) pi.nl = 8;
-    if (!pi.nl || pi.bits > 1024)
-        return fail(c, HB_EUNSUPPORTED, "primes above 1024 bits are not supported by this build");
+    if (!pi.nl) return fail(c, HB_EUNSUPPORTED, "primes above 2048 bits are not supported by this build");
     pi.ss = (u32)pi.bits / 8;
     pi.tw = (u32)(pi.bits + 7) / 8;
     return 0;
@@ -717,25 +722,43 @@ uint64_t hb_block_count(const uint8_t *p_be, size_t p_len, uint32_t sectors, uin
     return C ? len / C + 1 : 0;
 }
 
-int hb_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be,
-                size_t range_len, const uint64_t *xs, size_t n, uint8_t *out) {
+static int prf_eval_common(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be,
+                           size_t range_len, const uint64_t *xs, const uint8_t *digests, size_t n,
+                           uint8_t *out) {
     if (!c) return HB_EINVAL;
     if (int rc = check_key(c, key_len)) return rc;
     const int bits = bitlen_be(range_be, range_len);
     if (bits == 0) return fail(c, HB_EINVAL, "PRF range must be positive");
     const int nl = nl_for_bits(bits);
-    if (!nl) return fail(c, HB_EUNSUPPORTED, "PRF ranges above 1024 bits are not supported by this build");
+    if (!nl) return fail(c, HB_EUNSUPPORTED, "PRF ranges above 2048 bits are not supported by this build");
     if (n == 0) return 0;
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
-    HB_CHECK(c->xs.ensure(n * 8), "hipMalloc");
+    const u64 *xd = nullptr;
+    const u32 *dd = nullptr;
+    if (digests) {
+        // digests: n x 32 bytes (SHA-256 output order) -> big-endian words
+        std::vector<u32> w(n * 8);
+        for (size_t i = 0; i < n * 8; ++i)
+            w[i] = (u32)digests[4 * i] << 24 | (u32)digests[4 * i + 1] << 16 | (u32)digests[4 * i + 2] << 8 |
+                   digests[4 * i + 3];
+        HB_CHECK(c->xs.ensure(n * 32), "hipMalloc");
+        HB_CHECK(hipMemcpyAsync(c->xs.p, w.data(), n * 32, hipMemcpyHostToDevice, c->stream), "H2D");
+        HB_CHECK(hipStreamSynchronize(c->stream), "H2D(digests)");
+        dd = (const u32 *)c->xs.p;
+    } else {
+        HB_CHECK(c->xs.ensure(n * 8), "hipMalloc");
+        HB_CHECK(hipMemcpyAsync(c->xs.p, xs, n * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+        xd = (const u64 *)c->xs.p;
+    }
     HB_CHECK(c->vals.ensure(n * (size_t)nl * 4), "hipMalloc");
-    HB_CHECK(hipMemcpyAsync(c->xs.p, xs, n * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+    u32 *vd = (u32 *)c->vals.p;
     int rc = 0;
     switch (nl) {
-    case 2: rc = run_prf<2>(c, key, key_len, range_be, range_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6); break;
-    case 8: rc = run_prf<8>(c, key, key_len, range_be, range_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6); break;
-    case 16: rc = run_prf<16>(c, key, key_len, range_be, range_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6); break;
-    default: rc = run_prf<32>(c, key, key_len, range_be, range_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6); break;
+    case 2: rc = run_prf<2>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
+    case 8: rc = run_prf<8>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
+    case 16: rc = run_prf<16>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
+    case 32: rc = run_prf<32>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
+    default: rc = run_prf<64>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
     }
     if (rc) return rc;
     std::vector<u32> h(n * (size_t)nl);
@@ -747,6 +770,17 @@ int hb_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *ra
     return 0;
 }
 
+int hb_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be,
+                size_t range_len, const uint64_t *xs, size_t n, uint8_t *out) {
+    return prf_eval_common(c, key, key_len, range_be, range_len, xs, nullptr, n, out);
+}
+
+int hb_prf_eval_digests(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be,
+                        size_t range_len, const uint8_t *digests, size_t n, uint8_t *out) {
+    if (!digests && n) return fail(c, HB_EINVAL, "digests buffer is NULL");
+    return prf_eval_common(c, key, key_len, range_be, range_len, nullptr, digests, n, out);
+}
+
 int hb_cxx_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *limit_be,
                     size_t limit_len, const uint32_t *xs, size_t n, uint8_t *out) {
     if (!c) return HB_EINVAL;
@@ -755,7 +789,7 @@ int hb_cxx_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t
     if (bits == 0) return fail(c, HB_EINVAL, "PRF limit must be positive");
     const int nl = nl_for_bits(bits);
     const size_t nb = (size_t)(bits + 7) / 8;
-    if (!nl) return fail(c, HB_EUNSUPPORTED, "PRF limits above 1024 bits are not supported by this build");
+    if (!nl) return fail(c, HB_EUNSUPPORTED, "PRF limits above 2048 bits are not supported by this build");
     const int mode = nb % 16 ? 2 : 1;   // byte-granular CFB-128 unless whole blocks per try
     if (n == 0) return 0;
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
@@ -769,7 +803,8 @@ int hb_cxx_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t
     switch (nlv) {
     case 8: rc = run_prf<8>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
     case 16: rc = run_prf<16>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
-    default: rc = run_prf<32>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
+    case 32: rc = run_prf<32>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
+    default: rc = run_prf<64>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
     }
     if (rc) return rc;
     std::vector<u32> h(n * (size_t)nlv);
@@ -797,7 +832,8 @@ int hb_encode(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
     switch (pi.nl) {
     case 8: return encode_impl<8>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
     case 16: return encode_impl<16>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
-    default: return encode_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
+    case 32: return encode_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
+    default: return encode_impl<64>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
     }
 }
 
@@ -818,7 +854,8 @@ int hb_prove(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
     switch (pi.nl) {
     case 8: return prove_impl<8>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
     case 16: return prove_impl<16>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
-    default: return prove_impl<32>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    case 32: return prove_impl<32>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    default: return prove_impl<64>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
     }
 }
 
@@ -864,7 +901,8 @@ static int verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sec
     switch (pi.nl) {
     case 8: return verify_impl<8>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
     case 16: return verify_impl<16>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
-    default: return verify_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
+    case 32: return verify_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
+    default: return verify_impl<64>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
     }
 }
 
@@ -890,6 +928,21 @@ int hb_fill_random(hb_ctx *c, uint8_t *dev_ptr, uint64_t len, uint64_t seed) {
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     HB_CHECK(hb_launch_fill(dev_ptr, len, seed, c->stream), "hb_fill_kernel launch");
     HB_CHECK(hipStreamSynchronize(c->stream), "hb_fill_kernel");
+    return 0;
+}
+
+int hb_stream_read(hb_ctx *c, const void *dev_ptr, uint64_t len, double *ms) {
+    if (!c || !dev_ptr) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    if ((uintptr_t)dev_ptr % 16) return fail(c, HB_EINVAL, "hb_stream_read needs a 16-byte aligned buffer");
+    HB_CHECK(c->sums.ensure(64), "hipMalloc");
+    HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
+    HB_CHECK(hb_launch_read(dev_ptr, len, (u32 *)c->sums.p, c->num_cus, c->stream), "hb_read_kernel launch");
+    HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
+    HB_CHECK(hipEventSynchronize(c->k1), "hb_read_kernel");
+    float t = 0.f;
+    HB_CHECK(hipEventElapsedTime(&t, c->k0, c->k1), "hipEventElapsedTime");
+    if (ms) *ms = t;
     return 0;
 }
 

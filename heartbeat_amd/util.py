@@ -2,6 +2,7 @@
 KeyedPRF (:44-96), whose eval runs on the GPU (hb_prf_eval)."""
 import base64
 import ctypes
+import hashlib
 
 import numpy as np
 
@@ -58,18 +59,25 @@ class KeyedPRF(object):
         if rng <= 0:
             raise HeartbeatError("KeyedPRF range must be positive")
         xs = [int(x) for x in xs]
-        if any(x < 0 or x >= 1 << 64 for x in xs):
-            raise HeartbeatError("KeyedPRF inputs must be in [0, 2^64)")
         if not xs:
             return []
         key = _key_bytes(self.key)
         nb = (rng.bit_length() + 7) // 8
-        arr = np.asarray(xs, dtype=np.uint64)
         out = ctypes.create_string_buffer(nb * len(xs))
         ctx = _native.context()
         rb = _native.be(rng)
-        with ctx.lock:
-            ctx.check(_native.lib().hb_prf_eval(ctx.h, key, len(key), rb, len(rb),
-                                                arr.ctypes.data, len(xs), out))
+        if all(0 <= x < 1 << 64 for x in xs):
+            # the kernel hashes decimal(x) itself
+            arr = np.asarray(xs, dtype=np.uint64)
+            with ctx.lock:
+                ctx.check(_native.lib().hb_prf_eval(ctx.h, key, len(key), rb, len(rb),
+                                                    arr.ctypes.data, len(xs), out))
+        else:
+            # any other int (negative, wider than 64 bits): the reference hashes
+            # str(x) (util.py:91); hash on the host, run the PRF on the GPU
+            digs = b"".join(hashlib.sha256(str(x).encode()).digest() for x in xs)
+            with ctx.lock:
+                ctx.check(_native.lib().hb_prf_eval_digests(ctx.h, key, len(key), rb, len(rb),
+                                                            digs, len(xs), out))
         raw = out.raw
         return [int.from_bytes(raw[i * nb:(i + 1) * nb], "big") for i in range(len(xs))]

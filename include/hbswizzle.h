@@ -83,6 +83,15 @@ int hb_prf_eval(hb_ctx *ctx, const uint8_t *key, size_t key_len,
                 const uint8_t *range_be, size_t range_len,
                 const uint64_t *xs, size_t n, uint8_t *out);
 
+/* KeyedPRF.eval over caller-hashed inputs.
+ * Replaces heartbeat/util.py:83-96 for inputs hb_prf_eval cannot take: the
+ * reference hashes str(x) of ANY Python int (util.py:91), negative and wider
+ * than 64 bits included.  digests: n x 32 bytes, digest i = SHA256(str(x_i));
+ * out as hb_prf_eval. */
+int hb_prf_eval_digests(hb_ctx *ctx, const uint8_t *key, size_t key_len,
+                        const uint8_t *range_be, size_t range_len,
+                        const uint8_t *digests, size_t n, uint8_t *out);
+
 /* Swizzle encode of a run of blocks.
  * Replaces heartbeat/PySwizzle/PySwizzle.py:296-309 (the encode loop) and
  * cxx/shacham_waters_private.cxx:672-697.  For k in [0, nblocks):
@@ -103,7 +112,7 @@ int hb_encode(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
               uint64_t *tries_out);
 
 /* The cxx prf, prf::evaluate(i) (cxx/prf.hxx:125-145), for n unsigned-int
- * inputs, keyed by key and bounded by limit (any limit up to 1024 bits; when
+ * inputs, keyed by key and bounded by limit (any limit up to 2048 bits; when
  * ByteCount(limit) is not a multiple of 16 the CFB-128 stream continues
  * mid-block across tries): out receives n values of ByteCount(limit)
  * big-endian bytes each. */
@@ -187,6 +196,11 @@ int hb_host_unregister(hb_ctx *ctx, void *ptr);
  * the benchmarks and tests: byte k = byte (k mod 8) (little-endian) of
  * splitmix64(seed ^ (2*(k/16) + ((k mod 16) >= 8)) * 0xD1B54A32D192ED03). */
 int hb_fill_random(hb_ctx *ctx, uint8_t *dev_ptr, uint64_t len, uint64_t seed);
+
+/* Measurement helper (no reference counterpart): read len bytes of device
+ * memory once with streaming 16-byte loads; *ms = kernel time.  bench.py
+ * reports len / ms as the measured HBM read peak beside the vendor figure. */
+int hb_stream_read(hb_ctx *ctx, const void *dev_ptr, uint64_t len, double *ms);
 
 #ifdef __cplusplus
 }

@@ -31,6 +31,8 @@ def lib():
         L.hbo_encode.argtypes = [c.c_char_p, c.c_size_t, c.c_uint32, c.c_char_p, c.c_char_p,
                                  c.c_size_t, c.c_uint64, c.c_void_p, c.c_uint64, c.c_uint64,
                                  c.c_void_p, c.c_int]
+        L.hbo_prf_eval_dec.argtypes = [c.c_char_p, c.c_size_t, c.c_char_p, c.c_size_t,
+                                       c.c_char_p, c.c_char_p, c.c_size_t]
         L.hbo_cxx_prf_eval.argtypes = [c.c_char_p, c.c_size_t, c.c_char_p, c.c_size_t,
                                        c.c_uint32, c.c_char_p, c.c_size_t]
         L.hbo_cxx_encode.argtypes = L.hbo_encode.argtypes
@@ -69,11 +71,15 @@ def _addr(buf):
 
 
 def prf_eval(key, rng, x):
-    """KeyedPRF(key, rng).eval(x) (heartbeat/util.py:83-96)."""
+    """KeyedPRF(key, rng).eval(x) (heartbeat/util.py:83-96), any int x."""
     nb = (int(rng).bit_length() + 7) // 8
     out = ctypes.create_string_buffer(max(nb, 1))
     rb = _be(rng)
-    rc = lib().hbo_prf_eval(bytes(key), len(key), rb, len(rb), int(x), out, nb)
+    x = int(x)
+    if 0 <= x < (1 << 64):
+        rc = lib().hbo_prf_eval(bytes(key), len(key), rb, len(rb), x, out, nb)
+    else:
+        rc = lib().hbo_prf_eval_dec(bytes(key), len(key), rb, len(rb), str(x).encode(), out, nb)
     if rc <= 0:
         raise ValueError("oracle prf error %d" % rc)
     return int.from_bytes(out.raw[:nb], "big")

@@ -123,14 +123,13 @@ static void prf_free(prf_t *f) {
     BN_free(f->range);
 }
 
-/* KeyedPRF.eval(x) -> out (BIGNUM); returns number of tries. */
-static int prf_eval(prf_t *f, uint64_t x, BIGNUM *out) {
+/* KeyedPRF.eval of the message str(x) (dec, n bytes) -> out (BIGNUM);
+ * returns number of tries. */
+static int prf_eval_msg(prf_t *f, const char *dec, size_t n, BIGNUM *out) {
     static const unsigned char zero_iv[16] = {0};
     unsigned char digest[32], data[HBO_MAX_NB], ct[HBO_MAX_NB];
-    char dec[32];
-    int n, len, tries = 0;
-    n = snprintf(dec, sizeof dec, "%llu", (unsigned long long)x);   /* str(x) */
-    SHA256((const unsigned char *)dec, (size_t)n, digest);
+    int len, tries = 0;
+    SHA256((const unsigned char *)dec, n, digest);
     memset(data, 0, (size_t)f->nb);                                  /* KeyedPRF.pad */
     memcpy(data, digest, f->nb < 32 ? (size_t)f->nb : 32u);
     /* fresh cipher state per eval (util.py:88): reset the CFB-8 register */
@@ -142,6 +141,13 @@ static int prf_eval(prf_t *f, uint64_t x, BIGNUM *out) {
         BN_bin2bn(ct, f->nb, out);
         if (BN_cmp(out, f->range) < 0) return tries;
     }
+}
+
+/* KeyedPRF.eval(x) for 0 <= x < 2^64. */
+static int prf_eval(prf_t *f, uint64_t x, BIGNUM *out) {
+    char dec[32];
+    int n = snprintf(dec, sizeof dec, "%llu", (unsigned long long)x);   /* str(x) */
+    return prf_eval_msg(f, dec, (size_t)n, out);
 }
 
 /* prf::evaluate(i) (prf.hxx:125-145) -> out; returns number of tries. */
@@ -192,6 +198,23 @@ int hbo_prf_eval(const unsigned char *key, size_t keylen,
     if (rc) return rc;
     v = BN_new();
     tries = prf_eval(&f, x, v);
+    BN_bn2binpad(v, out_be, (int)out_len);
+    BN_free(v);
+    prf_free(&f);
+    return tries;
+}
+
+/* KeyedPRF.eval(x) for any Python int x given as its decimal string str(x)
+ * (util.py:91 hashes str(x), so negative and > 64-bit inputs are valid). */
+int hbo_prf_eval_dec(const unsigned char *key, size_t keylen,
+                     const unsigned char *range_be, size_t range_len,
+                     const char *dec, unsigned char *out_be, size_t out_len) {
+    prf_t f;
+    BIGNUM *v;
+    int tries, rc = prf_init(&f, key, keylen, range_be, range_len);
+    if (rc) return rc;
+    v = BN_new();
+    tries = prf_eval_msg(&f, dec, strlen(dec), v);
     BN_bn2binpad(v, out_be, (int)out_len);
     BN_free(v);
     prf_free(&f);
@@ -294,7 +317,7 @@ static int encode_mode(const unsigned char *p_be, size_t p_len, uint32_t sectors
     prf_t a;
     pthread_t *th;
     enc_job_t *jobs;
-    if (bits < 9 || sectors == 0) { BN_free(p); return -4; }
+    if (bits < 8 || sectors == 0) { BN_free(p); return -4; }
     alpha = (BIGNUM **)calloc(sectors, sizeof(BIGNUM *));
     rc = prf_init_mode(&a, a_key, keylen, p_be, p_len, mode);
     if (rc) { BN_free(p); free(alpha); return rc; }

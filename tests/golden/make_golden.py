@@ -272,5 +272,96 @@ def main():
         json.dump({k: hex(v) for k, v in PRIMES.items()}, fh, indent=1)
 
 
+def position_cases(sw):
+    """File-position semantics and prime sizes outside the main sweep.
+
+    * encode reads from the file's CURRENT position (PySwizzle.py:299) while
+      prove seeks ABSOLUTE offsets (PySwizzle.py:353-355): a BytesIO that
+      encode left at EOF, a file encoded from a mid position, a file proved
+      from a mid position;
+    * an 8-bit prime (sector size 1) and a 2048-bit prime (above the 1024-bit
+      default, PySwizzle.py:233,251);
+    * KeyedPRF inputs outside [0, 2^64): the reference hashes str(x) of any int
+      (util.py:91), negative numbers included.
+    """
+    beat_key = det_bytes("pyswizzle-state-key", 32)
+    cases = []
+
+    def flow(name, p, S, data, start, prove_pos, chunks2=7):
+        """encode from `start`, then prove on the SAME object positioned at
+        `prove_pos` (None: wherever encode left it, i.e. EOF)."""
+        f_key = det_bytes("f/" + name, 32)
+        a_key = det_bytes("a/" + name, 32)
+        iv = det_bytes("iv/" + name, 16)
+        chal_key = det_bytes("chal/" + name, 32)
+        beat = sw.PySwizzle(S, beat_key, p)
+        ShimRandom.reseed(name.encode())
+        ShimRandom.push(f_key, a_key, iv)
+        fh = io.BytesIO(data)
+        fh.seek(start)
+        tag, state = beat.encode(fh)
+        st = state.todict()                  # encrypted, as encode returns it
+        after_encode = fh.tell()
+        ShimRandom.push(chal_key)
+        chal = beat.gen_challenge(state)
+        if prove_pos is not None:
+            fh.seek(prove_pos)
+        proof = beat.prove(fh, chal, tag)
+        ok = beat.verify(proof, chal, state)
+        chal2 = sw.Challenge(chunks2, p, det_bytes("chal2/" + name, 32))
+        if prove_pos is not None:
+            fh.seek(prove_pos)
+        proof2 = beat.prove(fh, chal2, tag)
+        ok2 = beat.verify(proof2, chal2, state)
+        cases.append({
+            "name": name, "prime": hex(p), "sectors": S, "data": data.hex(),
+            "encode_start": start, "pos_after_encode": after_encode,
+            "prove_pos": prove_pos,
+            "f_key": f_key.hex(), "alpha_key": a_key.hex(), "state_key": beat_key.hex(),
+            "state": st, "tags": [hex(t) for t in tag.sigma],
+            "chal": {"chunks": chal.chunks, "v_max": hex(chal.v_max), "key": chal_key.hex()},
+            "proof": {"mu": [hex(m) for m in proof.mu], "sigma": hex(proof.sigma)}, "verifies": bool(ok),
+            "chal2": {"chunks": chunks2, "v_max": hex(p), "key": chal2.key.hex()},
+            "proof2": {"mu": [hex(m) for m in proof2.mu], "sigma": hex(proof2.sigma)},
+            "verifies2": bool(ok2),
+        })
+
+    p = PRIMES["p256"]
+    C = 3 * 32
+    d = det_bytes("pos/data", 5 * C + 7)
+    flow("pos/p256/eof", p, 3, d, 0, None)
+    flow("pos/p256/prove_mid", p, 3, d, 0, 37)
+    flow("pos/p256/encode_mid", p, 3, d, 100, None)
+    flow("pos/p256/encode_mid_prove0", p, 3, d, 100, 0)
+    flow("pos/p255/eof", PRIMES["p255"], 4, det_bytes("pos/data255", 9 * 31 * 4 + 30), 0, None, 40)
+    p8 = 251
+    for S in (1, 3):
+        for L in (0, 1, 2, 3, 5, 17):
+            flow("p8/S%d/L%d" % (S, L), p8, S, det_bytes("p8/%d/%d" % (S, L), L), 0, 0)
+    p2048 = seeded_prime("hb-golden-prime-2048", 2048)
+    for S in (1, 2):
+        for L in (0, 1, 255, 256, 257, 3 * 256 * S + 9):
+            flow("p2048/S%d/L%d" % (S, L), p2048, S, det_bytes("p2048/%d/%d" % (S, L), L), 0, 0)
+
+    prf = []
+    xs = [-1, -2, -10, -(1 << 64), -(10 ** 30), 1 << 64, (1 << 64) + 1, 1 << 100, 10 ** 30,
+          (1 << 128) - 1]
+    for r in (10000, PRIMES["p256"], p2048):
+        k = det_bytes("prf-key-32a", 32)
+        f = sw.KeyedPRF(k, r)
+        prf.append({"key": k.hex(), "range": str(r), "xs": [str(x) for x in xs],
+                    "outs": [str(f.eval(x)) for x in xs]})
+    with open(os.path.join(HERE, "position_cases.json"), "w") as fh:
+        json.dump({"generator": "tests/golden/make_golden.py --only position",
+                   "reference": "heartbeat/PySwizzle/PySwizzle.py:279-395, heartbeat/util.py:83-96",
+                   "p2048": hex(p2048), "cases": cases, "prf_wide_x": prf}, fh, indent=0)
+    print("position cases", len(cases))
+
+
 if __name__ == "__main__":
-    main()
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "position":
+        check_shim()
+        position_cases(load_reference())
+    else:
+        main()
+        position_cases(load_reference())

@@ -90,3 +90,50 @@ def test_cxx_prove_verifies_against_cxx_encode():
             rhs += O.cxx_prf_eval(ck, p, i)[0] * O.cxx_prf_eval(fk, p, idx)[0]
         rhs += sum(O.cxx_prf_eval(ak, p, j)[0] * mu[j] for j in range(S))
         assert sigma == rhs % p, chunks
+
+
+def test_position_cases(oracle):
+    """Reference semantics of the file position (encode reads from tell(),
+    prove seeks absolute offsets), 8-bit and 2048-bit primes."""
+    from conftest import load_golden
+    g = load_golden("position_cases.json")
+    for c in g["cases"]:
+        p = int(c["prime"], 16)
+        S = c["sectors"]
+        data = bytes.fromhex(c["data"])
+        fk, ak = bytes.fromhex(c["f_key"]), bytes.fromhex(c["alpha_key"])
+        tags = oracle.encode(p, S, fk, ak, data[c["encode_start"]:])
+        assert tags == [int(t, 16) for t in c["tags"]], c["name"]
+        for chn, prn, okn in (("chal", "proof", "verifies"), ("chal2", "proof2", "verifies2")):
+            ch = c[chn]
+            mu, sg = oracle.prove(p, S, bytes.fromhex(ch["key"]), ch["chunks"],
+                                  int(ch["v_max"], 16), tags, data)
+            assert mu == [int(m, 16) for m in c[prn]["mu"]], c["name"]
+            assert sg == int(c[prn]["sigma"], 16), c["name"]
+            assert oracle.verify(p, S, fk, ak, len(tags), bytes.fromhex(ch["key"]), ch["chunks"],
+                                 int(ch["v_max"], 16), mu, sg) == c[okn], c["name"]
+
+
+def test_prf_wide_inputs(oracle):
+    """KeyedPRF of negative and > 64-bit ints (the reference hashes str(x))."""
+    from conftest import load_golden
+    for c in load_golden("position_cases.json")["prf_wide_x"]:
+        key = bytes.fromhex(c["key"])
+        for x, o in zip(c["xs"], c["outs"]):
+            assert oracle.prf_eval(key, int(c["range"]), int(x)) == int(o), x
+
+
+def test_pure_python_port_matches_golden(golden_encode):
+    """oracle/pyswizzle_port.py (the single-core "PySwizzle" CPU baseline)."""
+    import io
+    from oracle import pyswizzle_port as PP
+    n = 0
+    for c in golden_encode["cases"]:
+        if c["len"] > 2000:
+            continue
+        p = int(c["prime"], 16)
+        tags = PP.encode(p, c["sectors"], bytes.fromhex(c["f_key"]), bytes.fromhex(c["alpha_key"]),
+                         io.BytesIO(bytes.fromhex(c["data"])))
+        assert tags == [int(t, 16) for t in c["tags"]], c["name"]
+        n += 1
+    assert n > 100
