@@ -49,24 +49,25 @@ hipError_t hb_launch_fill(unsigned char *dst, u64 len, u64 seed, hipStream_t s) 
 // Measured HBM read peak for the roofline (bench.py): every byte of the buffer
 // read once with 16-byte loads, four in flight per thread; an XOR fold keeps
 // the loads live.
-__global__ __launch_bounds__(256) void hb_read_kernel(const uint4 *src, u64 n16, u32 *sink) {
+typedef u32 hb_u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void hb_read_kernel(const hb_u32x4 *src, u64 n16, u32 *sink) {
     const u64 stride = (u64)gridDim.x * blockDim.x;
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    u32 acc = 0;
+    hb_u32x4 acc = {0, 0, 0, 0};
     for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride);
-        const uint4 c = __builtin_nontemporal_load(src + i + 2 * stride), d = __builtin_nontemporal_load(src + i + 3 * stride);
-        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+        const hb_u32x4 a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride);
+        const hb_u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+        const hb_u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
+        acc ^= a ^ b ^ c ^ d;
     }
-    for (; i < n16; i += stride) {
-        const uint4 a = src[i];
-        acc ^= a.x ^ a.y ^ a.z ^ a.w;
-    }
-    if (acc == 0x9e3779b9u) sink[0] = acc;   // practically never taken
+    for (; i < n16; i += stride) acc ^= src[i];
+    const u32 x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x9e3779b9u) sink[0] = x;   // practically never taken
 }
 
 hipError_t hb_launch_read(const void *src, u64 len, u32 *sink, int num_cus, hipStream_t s) {
-    hipLaunchKernelGGL(hb_read_kernel, dim3(num_cus * 16), dim3(256), 0, s, (const uint4 *)src, len / 16, sink);
+    hipLaunchKernelGGL(hb_read_kernel, dim3(num_cus * 16), dim3(256), 0, s, (const hb_u32x4 *)src, len / 16, sink);
     return hipGetLastError();
 }
 
