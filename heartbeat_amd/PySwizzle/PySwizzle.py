@@ -25,7 +25,7 @@ import os
 
 import numpy as np
 
-from .. import _native
+from .. import _native, multi
 from .._filebuf import FileBuffer
 from ..exc import HeartbeatError
 from ..util import KeyedPRF, hb_decode, hb_encode
@@ -304,20 +304,12 @@ class PySwizzle(object):
         # file.seek(pos) before every read (PySwizzle.py:353-355)
         fb = FileBuffer(file, from_start=True)
         try:
-            mu = ctypes.create_string_buffer(w * S)
-            sg = ctypes.create_string_buffer(w)
-            ctx = _native.context()
-            pb = _native.be(p)
             tarr = np.frombuffer(tags_raw, dtype=np.uint8)
-            with ctx.lock:
-                ctx.check(_native.lib().hb_prove(ctx.h, pb, len(pb), S, key, len(key), chunks,
-                                                 vmax, len(vmax), tarr.ctypes.data, ntags,
-                                                 fb.addr, fb.len, 0, mu, sg))
+            proof.mu, proof.sigma = multi.prove_shards(p, S, key, chunks, vmax, tarr.ctypes.data, ntags,
+                                                       fb.addr, fb.len, 0, multi.devices())
         finally:
             fb.restore()
             fb.close()
-        proof.mu = [int.from_bytes(mu.raw[j * w:(j + 1) * w], "big") for j in range(S)]
-        proof.sigma = int.from_bytes(sg.raw, "big")
         return proof
 
     def verify(self, proof, chal, state):
@@ -362,25 +354,22 @@ class PySwizzle(object):
         return Proof
 
 
-def encode_file(p, sectors, f_key, alpha_key, file):
-    """GPU encode of a file object / buffer: (Tag, number of blocks)."""
+def encode_file(p, sectors, f_key, alpha_key, file, devices=None):
+    """GPU encode of a file object / buffer: (Tag, number of blocks).  Files of
+    at least 2 x multi.MIN_SHARD_BYTES are sharded by block range over
+    `devices` (default: multi.devices(), every visible GPU)."""
     w = _native.width_of(p)
     ss = p.bit_length() // 8
     C = ss * sectors
+    fk, ak = _kb(f_key), _kb(alpha_key)
+    if len(fk) != len(ak):
+        raise HeartbeatError("f_key and alpha_key must have the same length")
     fb = FileBuffer(file)
     try:
         nblocks = fb.len // C + 1
         out = np.empty(nblocks * w, dtype=np.uint8)
-        ctx = _native.context()
-        pb = _native.be(p)
-        fk, ak = _kb(f_key), _kb(alpha_key)
-        if len(fk) != len(ak):
-            raise HeartbeatError("f_key and alpha_key must have the same length")
-        tries = ctypes.c_uint64(0)
-        with ctx.lock:
-            ctx.check(_native.lib().hb_encode(ctx.h, pb, len(pb), sectors, fk, ak, len(fk), 0,
-                                              fb.addr, fb.len, nblocks, out.ctypes.data, 0,
-                                              ctypes.byref(tries)))
+        multi.encode_shards(p, sectors, fk, ak, fb.addr, fb.len, nblocks, out.ctypes.data, 0,
+                            multi.devices(devices))
         fb.consume()
     finally:
         fb.close()

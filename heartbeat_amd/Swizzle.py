@@ -19,7 +19,7 @@ import ctypes
 
 import numpy as np
 
-from . import _native
+from . import _native, multi
 from ._filebuf import FileBuffer
 from .exc import HeartbeatError
 from .PySwizzle.PySwizzle import Challenge, Proof, State, Tag, _kb, _random_bytes, getPrime
@@ -93,12 +93,8 @@ class Swizzle(object):
         try:
             nblocks = fb.len // C + 1
             out = np.empty(nblocks * w, dtype=np.uint8)
-            ctx = _native.context()
-            pb = _native.be(p)
-            with ctx.lock:
-                ctx.check(_native.lib().hb_encode(ctx.h, pb, len(pb), self.sectors, state.f_key,
-                                                  state.alpha_key, 32, 0, fb.addr, fb.len, nblocks,
-                                                  out.ctypes.data, _native.HB_PRF_CXX, None))
+            multi.encode_shards(p, self.sectors, state.f_key, state.alpha_key, fb.addr, fb.len, nblocks,
+                                out.ctypes.data, _native.HB_PRF_CXX, multi.devices())
             fb.consume()
         finally:
             fb.close()
@@ -136,22 +132,14 @@ class Swizzle(object):
         key = _kb(chal.key)
         vmax = _native.be(int(chal.v_max))
         # absolute offsets from the start of the file, as the reference's
-        # file.seek(pos) before every read (PySwizzle.py:353-355)
+        # f.seek(pos) before every read (shacham_waters_private.cxx:763-764)
         fb = FileBuffer(file, from_start=True)
         try:
-            mu = ctypes.create_string_buffer(w * S)
-            sg = ctypes.create_string_buffer(w)
-            ctx = _native.context()
-            pb = _native.be(p)
-            with ctx.lock:
-                ctx.check(_native.lib().hb_prove(ctx.h, pb, len(pb), S, key, len(key), chunks, vmax,
-                                                 len(vmax), tarr.ctypes.data, ntags, fb.addr, fb.len,
-                                                 _native.HB_PRF_CXX, mu, sg))
+            proof.mu, proof.sigma = multi.prove_shards(p, S, key, chunks, vmax, tarr.ctypes.data, ntags,
+                                                       fb.addr, fb.len, _native.HB_PRF_CXX, multi.devices())
         finally:
             fb.restore()
             fb.close()
-        proof.mu = [int.from_bytes(mu.raw[j * w:(j + 1) * w], "big") for j in range(S)]
-        proof.sigma = int.from_bytes(sg.raw, "big")
         return proof
 
     def verify(self, proof, chal, state):

@@ -32,6 +32,7 @@ _P = _c.c_void_p
 _B = _c.c_char_p
 SIGNATURES = [
     ("hb_abi_version", _c.c_int, []),
+    ("hb_device_count", _c.c_int, [_c.POINTER(_c.c_int)]),
     ("hb_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_P)]),
     ("hb_ctx_destroy", None, [_P]),
     ("hb_last_error", _c.c_char_p, [_P]),
@@ -44,6 +45,9 @@ SIGNATURES = [
     ("hb_block_count", _c.c_uint64, [_B, _c.c_size_t, _c.c_uint32, _c.c_uint64]),
     ("hb_prove", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _c.c_size_t, _c.c_uint64, _B,
                             _c.c_size_t, _P, _c.c_uint64, _P, _c.c_uint64, _c.c_uint32, _P, _P]),
+    ("hb_prove_range", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _c.c_size_t, _c.c_uint64,
+                                  _c.c_uint64, _c.c_uint64, _B, _c.c_size_t, _P, _c.c_uint64, _P,
+                                  _c.c_uint64, _c.c_uint32, _P, _P]),
     ("hb_verify_rhs", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint32, _B, _B, _c.c_size_t,
                                  _c.c_uint64, _B, _c.c_size_t, _c.c_uint64, _B, _c.c_size_t,
                                  _B, _P]),
@@ -119,17 +123,20 @@ class Context(object):
             self.h = None
 
 
-def context(device=None):
-    """The process-wide context for `device` (default: $HB_DEVICE, $LOCAL_RANK or 0)."""
+def context(device=None, instance=0):
+    """The process-wide context for `device` (default: $HB_DEVICE, $LOCAL_RANK
+    or 0); `instance` > 0 opens further independent contexts on the same
+    device (multi.py uses them for repeated device entries)."""
     d = default_device() if device is None else int(device)
-    c = _ctxs.get(d)
+    key = (d, int(instance))
+    c = _ctxs.get(key)
     if c is None:
         lib()
         with _ctx_lock:
-            c = _ctxs.get(d)
+            c = _ctxs.get(key)
             if c is None:
                 c = Context(d)
-                _ctxs[d] = c
+                _ctxs[key] = c
     return c
 
 

@@ -77,34 +77,48 @@ struct MontArgs {
     u64 n;
 };
 
-// Weighted sums  sum_i w_i * value_{col}(i)  mod p  (w_i in Montgomery form).
-//   mode 0 (prove, device-resident file):  col < S -> sector col of block idx[i]
-//           of data; col == S -> tag idx[i] (tw big-endian bytes)
-//   mode 1 (verify): single column, value = vals[i] (NL limbs)
-//   mode 2 (prove, host-gathered blocks):  as mode 0 with block i of the
-//           gathered buffer (blen[i] valid bytes) and gathered tag i
+// Prove stage 1 (hb_prove_prf_kernel): the challenge's PRFs for indices
+// i0 .. i0+n-1.
+template <int NL>
+struct ProveArgs {
+    PrfParams<2> pi;              // idx = KeyedPRF(key, #tags) (cxx: prf with limit #tags)
+    PrfParams<NL> pv;             // v = KeyedPRF(key, v_max)
+    ModP<NL> mod;
+    u32 r2[NL];                   // R^2 mod p: v -> v R mod p
+    u64 i0, n, ntags;
+    u32 check_all;                // cxx prove, chunks >= #tags: idx_i = i, no index PRF
+    u64 *idx;                     // n block indices
+    u32 *vm;                      // n * NL limbs: v_i R mod p
+    const u32 *t0;
+    unsigned long long *queue;    // 2 slots: index engine, v engine
+    unsigned int *flags;          // bit 0: an index >= #tags (cxx prf after 81 tries)
+};
+
+// Weighted sums  sum_i w_i * value_{col}(i)  mod p  (w_i in Montgomery form);
+// modes: see hb_wsum_kernel.
+#define HB_WSUM_WG 256
 template <int NL>
 struct WsumArgs {
     ModP<NL> mod;
     u32 mode, ncols;
-    const u64 *idx;
+    const u64 *idx;               // mode 0: block of term i (nullptr: idx_base + i)
+    u64 idx_base;
+    u64 ntags;                    // mode 0: terms with idx >= ntags read as 0
     const u32 *w;
     u64 nterms;
     const unsigned char *data;
     u64 len, C;
     u32 ss, S, tw;
-    u32 wrap32;                   // cxx prove: block offset = (unsigned int)(idx * C)
-                                  // (shacham_waters_private.cxx:738, 763)
+    u32 wrap32;                   // cxx prove: offset = (unsigned int)(idx * C + j * ss)
+                                  // (shacham_waters_private.cxx:738, 762-763)
     const unsigned char *tags;
     const u32 *vals;
-    const u64 *blen;
-    u32 *partials;                // [ncols][nthreads][NL]
-};
-
-template <int NL>
-struct SumArgs {
-    ModP<NL> mod;
-    const u32 *partials;          // [ncols][nparts][NL], each < p
-    u32 nparts;
-    u32 *out;                     // [ncols][NL]
+    u32 *partials;                // [ncols][gridDim.x][NL]
+    unsigned int *ctl;            // ncols + 1 counters, zero between launches
+    u32 *out;                     // [ncols][NL] results, then one status word
+    u32 accumulate;               // out[col] += this launch's sum
+    u32 finalize;                 // record + zero the PRF slots and flags
+    unsigned long long *qslots;   // nslots PRF engine slots (HB_QSLOT counters each)
+    u32 nslots;
+    unsigned int *flags;
 };

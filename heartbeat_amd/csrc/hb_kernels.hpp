@@ -4,9 +4,10 @@
 //   hb_encode_kernel   tags of a run of blocks     (PySwizzle.py:296-309)
 //   hb_prf_kernel      batched KeyedPRF.eval        (util.py:83-96)
 //   hb_mont_kernel     x -> x R mod p (Montgomery form of alpha_j, v_i)
-//   hb_wsum_kernel     per-thread partial sums of w_i * value(i) for prove /
-//                      verify (PySwizzle.py:351-368, :388-394)
-//   hb_sum_kernel      mod-p tree reduction of the partials
+//   hb_prove_prf_kernel  prove stage 1: index and v PRFs of a challenge
+//   hb_wsum_kernel     weighted sums sum_i w_i * value(i) mod p for prove /
+//                      verify (PySwizzle.py:351-368, :388-394), finished in
+//                      the same launch by the last workgroup of each column
 //   hb_fill_kernel     synthetic file bytes (SplitMix64), benches and tests
 //
 // PRF engine.  KeyedPRF.eval is rejection sampling (E[tries] = 2^bitlen(R)/R,
@@ -412,7 +413,57 @@ __global__ __launch_bounds__(256) void hb_mont_kernel(MontArgs<NL> A) {
     for (int t = 0; t < NL; ++t) A.out[i * NL + t] = y[t];
 }
 
-// ------------------------------------------------------------------ prove / verify sums
+// ------------------------------------------------------------------ prove stage 1: PRFs
+// idx_i = KeyedPRF(key, #tags)(i0 + i) and v_i = KeyedPRF(key, v_max)(i0 + i)
+// (PySwizzle.py:344-345, 353, 357; cxx shacham_waters_private.cxx:742-748,
+// 762, 767) for i < n in ONE launch: two engine runs over the same LDS image,
+// v stored in Montgomery form (v R mod p) for stage 2.  check_all (cxx prove
+// with a challenge covering every block, :754-762) skips the index PRF.
+template <int NL>
+struct ProveIdxHandler {
+    const ProveArgs<NL> &A;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return A.i0 + job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void accept(u64 job, const u32 v[2]) const {
+        const u64 ix = (u64)v[0] | ((u64)v[1] << 32);
+        A.idx[job] = ix;
+        // the cxx prf returns a value >= the limit after 81 tries (prf.hxx:142),
+        // on which the reference's t.sigma().at(index) throws: flagged here,
+        // raised by the host; stage 2 reads such a term as 0
+        if (ix >= A.ntags) atomicOr(A.flags, 1u);
+    }
+};
+
+template <int NL>
+struct ProveVHandler {
+    const ProveArgs<NL> &A;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return A.i0 + job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void accept(u64 job, const u32 v[NL]) const {
+        u32 y[NL];
+        hb_to_mont<NL>(v, A.r2, A.mod, y);
+        u32 *o = A.vm + job * NL;
+        for (int t = 0; t < NL; ++t) o[t] = y[t];
+    }
+};
+
+template <int NL, int NR, int MODE_I, int MODE_V>
+__global__ __launch_bounds__(HB_ENGINE_WG) void hb_prove_prf_kernel(ProveArgs<NL> A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L = hb_lane_tab(lds);
+    if (!A.check_all) {
+        ProveIdxHandler<NL> hi{A};
+        hb_engine<2, NR, ProveIdxHandler<NL>, MODE_I>(hi, L, A.pi, A.n, A.queue);
+    }
+    ProveVHandler<NL> hv{A};
+    hb_engine<NL, NR, ProveVHandler<NL>, MODE_V>(hv, L, A.pv, A.n, A.queue + HB_QSLOT);
+}
+
+// ------------------------------------------------------------------ prove stage 2 / verify: weighted sums
+// Sector value at absolute offset pos: BE(data[pos : min(pos + ss, len)]),
+// 0 past EOF -- a short (last) sector is right-aligned, and the reference's
+// break after a short read (PySwizzle.py:359-360) only skips sectors past EOF.
 template <int NL, int ALIGN>
 __device__ __forceinline__ void hb_sector_value(const unsigned char *data, u64 len, u64 pos,
                                                 u32 ss, u32 m[NL]) {
@@ -426,8 +477,39 @@ __device__ __forceinline__ void hb_sector_value(const unsigned char *data, u64 l
     }
 }
 
+// r (NL limbs, < p) += x (NL limbs, < p) mod p
+template <int NL>
+__device__ __forceinline__ void hb_add_mod(u32 r[NL], const u32 *x, const ModP<NL> &M) {
+    u32 v[NL + 1], o[NL];
+    u64 c = 0;
+    for (int t = 0; t < NL; ++t) {
+        c += (u64)r[t] + x[t];
+        v[t] = (u32)c;
+        c >>= 32;
+    }
+    v[NL] = (u32)c;
+    hb_reduce_small<NL>(v, M, o);
+    for (int t = 0; t < NL; ++t) r[t] = o[t];
+}
+
+// column col of the weighted sum, term i:  w_i * value_col(i)
+//   mode 0 (prove, device-resident file): col < S -> sector col of block idx_i
+//          (absolute offset idx_i*C + col*ss, unsigned int arithmetic in the
+//          cxx prove, :762-763), col == S -> tag idx_i
+//   mode 1 (verify): single column, value = vals[i]
+//   mode 2 (prove, host-gathered batch): sector col of gathered block i (full
+//          ss-byte big-endian integers), col == S -> gathered tag i
+// Each thread accumulates its terms exactly (2NL+1 limbs) and reduces once;
+// a workgroup tree-reduces its residues; the last workgroup of each column
+// (agent-scope counter) adds the column's partials into out[col] (or onto it,
+// `accumulate`, for host batches after the first).  The call with `finalize`
+// also records the PRF engines' abandoned-job counts and the index flags in
+// out[ncols*NL] and zeroes the counters for the next operation: a prove is
+// two launches with no memset.
 template <int NL, int ALIGN>
-__global__ __launch_bounds__(256) void hb_wsum_kernel(WsumArgs<NL> A) {
+__global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
+    __shared__ u32 sh[HB_WSUM_WG * NL];
+    __shared__ unsigned int last;
     const u32 col = blockIdx.y;
     const u64 tid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     const u64 nthreads = (u64)gridDim.x * blockDim.x;
@@ -437,15 +519,16 @@ __global__ __launch_bounds__(256) void hb_wsum_kernel(WsumArgs<NL> A) {
     for (u64 i = tid; i < A.nterms; i += nthreads) {
         if (A.mode == 1) {
             for (int t = 0; t < NL; ++t) m[t] = A.vals[i * NL + t];
+        } else if (A.mode == 2) {
+            if (col < A.S) hb_load_full16_or_bytes<NL, ALIGN>(A.data, i * A.C + (u64)col * A.ss, A.ss, m);
+            else hb_load_be_bytes<NL>(A.tags, i * A.tw, A.tw, m);
         } else {
-            const bool gathered = A.mode == 2;
-            const u64 blk = gathered ? i : A.idx[i];
-            if (col < A.S) {
-                const u64 blen = gathered ? A.blen[i] : A.len;
-                const u64 base = gathered ? i * A.C : A.wrap32 ? (u64)(u32)(blk * A.C) : blk * A.C;
-                const u64 pos = base + (u64)col * A.ss;
-                const u64 end = gathered ? base + blen : A.len;
-                hb_sector_value<NL, ALIGN>(A.data, end, pos, A.ss, m);
+            const u64 blk = A.idx ? A.idx[i] : A.idx_base + i;
+            if (blk >= A.ntags) {
+                for (int t = 0; t < NL; ++t) m[t] = 0;
+            } else if (col < A.S) {
+                const u64 pos = A.wrap32 ? (u64)(u32)(blk * A.C + (u64)col * A.ss) : blk * A.C + (u64)col * A.ss;
+                hb_sector_value<NL, ALIGN>(A.data, A.len, pos, A.ss, m);
             } else {
                 hb_load_be_bytes<NL>(A.tags, blk * A.tw, A.tw, m);
             }
@@ -455,47 +538,59 @@ __global__ __launch_bounds__(256) void hb_wsum_kernel(WsumArgs<NL> A) {
     u32 v[NL + 1], r[NL];
     hb_redc<NL>(acc, A.mod, v);
     hb_reduce_small<NL>(v, A.mod, r);
-    u32 *o = A.partials + ((u64)col * nthreads + tid) * NL;
-    for (int t = 0; t < NL; ++t) o[t] = r[t];
-}
-
-// one workgroup per column: sum nparts residues mod p
-template <int NL>
-__global__ __launch_bounds__(256) void hb_sum_kernel(SumArgs<NL> A) {
-    __shared__ u32 sh[256 * NL];
-    const u32 col = blockIdx.x;
-    u32 v[NL + 1];
-    for (int t = 0; t <= NL; ++t) v[t] = 0;
-    for (u32 k = threadIdx.x; k < A.nparts; k += blockDim.x) {
-        const u32 *x = A.partials + ((u64)col * A.nparts + k) * NL;
-        u64 c = 0;
-        for (int t = 0; t < NL; ++t) {
-            c += (u64)v[t] + x[t];
-            v[t] = (u32)c;
-            c >>= 32;
-        }
-        v[NL] += (u32)c;
-    }
-    u32 r[NL];
-    hb_reduce_small<NL>(v, A.mod, r);
+    // workgroup tree reduction mod p
     for (int t = 0; t < NL; ++t) sh[threadIdx.x * NL + t] = r[t];
     __syncthreads();
-    for (u32 s = blockDim.x / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            u32 w[NL + 1];
-            u64 c = 0;
-            for (int t = 0; t < NL; ++t) {
-                c += (u64)sh[threadIdx.x * NL + t] + sh[(threadIdx.x + s) * NL + t];
-                w[t] = (u32)c;
-                c >>= 32;
-            }
-            w[NL] = (u32)c;
-            hb_reduce_small<NL>(w, A.mod, r);
+    for (u32 sft = blockDim.x / 2; sft > 0; sft >>= 1) {
+        if (threadIdx.x < sft) {
+            for (int t = 0; t < NL; ++t) r[t] = sh[threadIdx.x * NL + t];
+            hb_add_mod<NL>(r, sh + (threadIdx.x + sft) * NL, A.mod);
             for (int t = 0; t < NL; ++t) sh[threadIdx.x * NL + t] = r[t];
         }
         __syncthreads();
     }
-    if (threadIdx.x < NL) A.out[col * NL + threadIdx.x] = sh[threadIdx.x];
+    u32 *part = A.partials + ((u64)col * gridDim.x + blockIdx.x) * NL;
+    if (threadIdx.x < NL) part[threadIdx.x] = sh[threadIdx.x];
+    __syncthreads();
+    // the last workgroup of this column finishes it (release / acquire at agent scope)
+    if (threadIdx.x == 0) {
+        const unsigned int k = __hip_atomic_fetch_add(A.ctl + col, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = k + 1 == gridDim.x;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) {
+        u32 sum[NL];
+        const u32 *o = A.out + (u64)col * NL;
+        for (int t = 0; t < NL; ++t) sum[t] = A.accumulate ? o[t] : 0u;
+        for (u32 b = 0; b < gridDim.x; ++b) {
+            const u32 *pp = A.partials + ((u64)col * gridDim.x + b) * NL;
+            u32 x[NL];
+            for (int t = 0; t < NL; ++t) x[t] = __hip_atomic_load(pp + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hb_add_mod<NL>(sum, x, A.mod);
+        }
+        for (int t = 0; t < NL; ++t) A.out[(u64)col * NL + t] = sum[t];
+        A.ctl[col] = 0;
+        // the last column to finish closes the operation
+        const unsigned int d = __hip_atomic_fetch_add(A.ctl + A.ncols, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (d + 1 == A.ncols) {
+            A.ctl[A.ncols] = 0;
+            if (A.finalize) {
+                u32 st = 0;
+                for (u32 s = 0; s < A.nslots; ++s) {
+                    unsigned long long *q = A.qslots + (u64)s * HB_QSLOT;
+                    st |= q[2] ? 2u : 0u;
+                    for (int k2 = 0; k2 < HB_QSLOT; ++k2) q[k2] = 0;
+                }
+                if (A.flags) {
+                    st |= *A.flags;
+                    *A.flags = 0;
+                }
+                A.out[(u64)A.ncols * NL] = st;
+            }
+            __threadfence();
+        }
+    }
 }
 
 // ------------------------------------------------------------------ launchers
@@ -552,15 +647,28 @@ hipError_t hb_launch_mont(const MontArgs<NL> &A, hipStream_t s) {
 
 template <int NL>
 hipError_t hb_launch_wsum(const WsumArgs<NL> &A, int align, int gridx, hipStream_t s) {
-    dim3 g(gridx, A.ncols), b(256);
+    dim3 g(gridx, A.ncols), b(HB_WSUM_WG);
     if (align == 16) hipLaunchKernelGGL((hb_wsum_kernel<NL, 16>), g, b, 0, s, A);
     else hipLaunchKernelGGL((hb_wsum_kernel<NL, 1>), g, b, 0, s, A);
     return hipGetLastError();
 }
 
+// stage 1 of prove; mode_i / mode_v: PRF modes of the index and v PRFs
+// (0 KeyedPRF; cxx prf: 1 whole blocks per try, 2 any limit)
 template <int NL>
-hipError_t hb_launch_sum(const SumArgs<NL> &A, int ncols, hipStream_t s) {
-    hipLaunchKernelGGL((hb_sum_kernel<NL>), dim3(ncols), dim3(256), 0, s, A);
+hipError_t hb_launch_prove_prf(const ProveArgs<NL> &A, int nr, int mode_i, int mode_v, int grid, hipStream_t s) {
+    dim3 g(grid), b(HB_ENGINE_WG);
+#define HB_PP(MI, MV)                                                                          \
+    do {                                                                                       \
+        if (nr == 14) hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 14, MI, MV>), g, b, 0, s, A); \
+        else if (nr == 12) hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 12, MI, MV>), g, b, 0, s, A); \
+        else hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 10, MI, MV>), g, b, 0, s, A);         \
+    } while (0)
+    if (mode_i == 0 && mode_v == 0) HB_PP(0, 0);
+    else if (mode_v == 2) HB_PP(2, 2);
+    else if constexpr (NL >= 4) HB_PP(2, 1);
+    else return hipErrorInvalidValue;
+#undef HB_PP
     return hipGetLastError();
 }
 
@@ -569,4 +677,4 @@ hipError_t hb_launch_sum(const SumArgs<NL> &A, int ncols, hipStream_t s) {
     template hipError_t hb_launch_prf<NL>(const PrfArgs<NL> &, int, int, int, hipStream_t);      \
     template hipError_t hb_launch_mont<NL>(const MontArgs<NL> &, hipStream_t);                   \
     template hipError_t hb_launch_wsum<NL>(const WsumArgs<NL> &, int, int, hipStream_t);         \
-    template hipError_t hb_launch_sum<NL>(const SumArgs<NL> &, int, hipStream_t);
+    template hipError_t hb_launch_prove_prf<NL>(const ProveArgs<NL> &, int, int, int, int, hipStream_t);

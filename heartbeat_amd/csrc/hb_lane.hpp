@@ -747,6 +747,13 @@ HB_HD void hb_load_full16(const unsigned char *data, u64 off, u32 m[NL]) {
     }
 }
 
+// A whole ss-byte sector at data + off (ALIGN = 16: full-width, 16-byte aligned).
+template <int NL, int ALIGN>
+HB_HD void hb_load_full16_or_bytes(const unsigned char *data, u64 off, u32 ss, u32 m[NL]) {
+    if (ALIGN == 16) hb_load_full16<NL>(data, off, m);
+    else hb_load_be_bytes<NL>(data, off, ss, m);
+}
+
 template <int NL>
 #ifndef HB_GROUP8
 #define HB_GROUP8 2

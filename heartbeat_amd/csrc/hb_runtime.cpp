@@ -28,7 +28,7 @@ hipError_t hb_launch_prefix(const PrefixArgs &, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_prf(const PrfArgs<NL> &, int, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_mont(const MontArgs<NL> &, hipStream_t);
 template <int NL> hipError_t hb_launch_wsum(const WsumArgs<NL> &, int, int, hipStream_t);
-template <int NL> hipError_t hb_launch_sum(const SumArgs<NL> &, int, hipStream_t);
+template <int NL> hipError_t hb_launch_prove_prf(const ProveArgs<NL> &, int, int, int, int, hipStream_t);
 hipError_t hb_launch_fill(unsigned char *, u64, u64, hipStream_t);
 hipError_t hb_launch_read(const void *, u64, u32 *, int, hipStream_t);
 
@@ -67,6 +67,10 @@ struct hb_ctx {
     unsigned long long *queue = nullptr;   // 16 slots of HB_QSLOT counters
     DevBuf alpha_raw, alpha_mont, xs, vals, vals2, wts, idx, partials, sums, data[2], tags, blen, gtags;
     DevBuf pfx, retry;   // two-pass encode: CFB prefix image, retry list
+    DevBuf ctl;          // wsum column counters + flags (zero between operations)
+    bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
+    u32 *hres = nullptr; // pinned host copy of wsum results (+ status)
+    size_t hres_n = 0;
     std::string err;
     double last_ms = 0.0;
     u32 last_launches = 0;
@@ -392,28 +396,65 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 }
 
 // ------------------------------------------------------------------ sums
-// Finish a wsum launch: reduce the partials of each column and return the
-// results as big-endian tw-byte values in out (host).
-template <int NL>
-int finish_sums(hb_ctx *c, const Limbs &p, u32 ncols, u32 nparts, u32 tw, uint8_t *out) {
-    SumArgs<NL> A;
-    make_mod<NL>(p, A.mod);
-    A.partials = (const u32 *)c->partials.p;
-    A.nparts = nparts;
-    HB_CHECK(c->sums.ensure((size_t)ncols * NL * 4), "hipMalloc");
-    A.out = (u32 *)c->sums.p;
-    HB_CHECK(hb_launch_sum<NL>(A, (int)ncols, c->stream), "hb_sum_kernel launch");
-    std::vector<u32> h((size_t)ncols * NL);
-    HB_CHECK(hipMemcpyAsync(h.data(), c->sums.p, h.size() * 4, hipMemcpyDeviceToHost, c->stream), "hipMemcpy");
-    HB_CHECK(hipStreamSynchronize(c->stream), "sum");
-    for (u32 k = 0; k < ncols; ++k) to_be(&h[(size_t)k * NL], NL, out + (size_t)k * tw, tw);
-    return check_prf_slots(c);
+// Column counters (ncols + 1) and the index flag word of hb_wsum_kernel,
+// zero on allocation; the kernels leave them zero.
+int ensure_ctl(hb_ctx *c, u32 ncols) {
+    const size_t want = ((size_t)ncols + 2) * sizeof(unsigned int);
+    if (c->ctl.n < want) {
+        HB_CHECK(c->ctl.ensure(want < 4096 ? 4096 : want), "hipMalloc(ctl)");
+        HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync(ctl)");
+    }
+    return 0;
+}
+
+unsigned int *flags_word(hb_ctx *c) { return (unsigned int *)c->ctl.p + (c->ctl.n / sizeof(unsigned int) - 1); }
+
+int ensure_hres(hb_ctx *c, size_t words) {
+    if (c->hres_n >= words) return 0;
+    if (c->hres) (void)hipHostFree(c->hres);
+    c->hres = nullptr;
+    c->hres_n = 0;
+    HB_CHECK(hipHostMalloc((void **)&c->hres, words * 4, 0), "hipHostMalloc");
+    c->hres_n = words;
+    return 0;
 }
 
 u32 wsum_grid(u64 nterms) {
-    u64 g = (nterms + 255) / 256;
-    if (g > 1024) g = 1024;
+    // >= 8 terms per thread before a second workgroup per column is worth it
+    u64 g = (nterms + 8 * HB_WSUM_WG - 1) / (8 * HB_WSUM_WG);
+    if (g > 128) g = 128;
     return (u32)(g ? g : 1);
+}
+
+// Launch a weighted-sum pass with results in c->sums (ncols * NL + status).
+template <int NL>
+int launch_wsum(hb_ctx *c, WsumArgs<NL> &A, int align) {
+    const u32 gx = wsum_grid(A.nterms);
+    HB_CHECK(c->partials.ensure((size_t)A.ncols * gx * NL * 4), "hipMalloc(partials)");
+    HB_CHECK(c->sums.ensure(((size_t)A.ncols * NL + 1) * 4), "hipMalloc(sums)");
+    if (int rc = ensure_ctl(c, A.ncols)) return rc;
+    A.partials = (u32 *)c->partials.p;
+    A.ctl = (unsigned int *)c->ctl.p;
+    A.flags = flags_word(c);
+    A.out = (u32 *)c->sums.p;
+    HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");
+    return 0;
+}
+
+// After the finalizing wsum: copy the results back (one D2H), check the
+// status word, write the ncols values big-endian (tw bytes each) to out.
+template <int NL>
+int finish_sums(hb_ctx *c, u32 ncols, u32 tw, uint8_t *out, bool cxx_index_check) {
+    const size_t words = (size_t)ncols * NL + 1;
+    if (int rc = ensure_hres(c, words)) return rc;
+    HB_CHECK(hipMemcpyAsync(c->hres, c->sums.p, words * 4, hipMemcpyDeviceToHost, c->stream), "hipMemcpy");
+    HB_CHECK(hipStreamSynchronize(c->stream), "prove");
+    const u32 st = c->hres[(size_t)ncols * NL];
+    if (st & 2u) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate");
+    if ((st & 1u) && cxx_index_check)
+        return fail(c, HB_EINVAL, "vector::_M_range_check: challenge index out of range");
+    for (u32 k = 0; k < ncols; ++k) to_be(&c->hres[(size_t)k * NL], NL, out + (size_t)k * tw, tw);
+    return 0;
 }
 
 int u64_be(u64 v, uint8_t out[8]) {
@@ -422,149 +463,187 @@ int u64_be(u64 v, uint8_t out[8]) {
 }
 
 // ------------------------------------------------------------------ prove
+// Host-data gather: the sectors of challenged blocks as full ss-byte
+// big-endian integers (a short last sector right-aligned, past EOF zero) --
+// the reference's seek(pos) / read(ss) per sector (PySwizzle.py:353-355,
+// cxx :763-765), offsets in unsigned int for the cxx prove.
+struct Gather {
+    const uint8_t *data;
+    u64 len, C;
+    u32 ss, S, tw;
+    bool wrap32;
+    const uint8_t *tags;
+    void run(const u64 *idx, u64 n, uint8_t *blocks, uint8_t *gtags) const {
+        for (u64 i = 0; i < n; ++i) {
+            const u64 ix = idx[i];
+            uint8_t *dst = blocks + i * C;
+            const u64 base = ix * C;
+            if (!wrap32 && base + C <= len) {
+                memcpy(dst, data + base, (size_t)C);
+            } else {
+                for (u32 j = 0; j < S; ++j) {
+                    const u64 pos = wrap32 ? (u64)(u32)(base + (u64)j * ss) : base + (u64)j * ss;
+                    const u64 r = pos >= len ? 0 : (len - pos < ss ? len - pos : ss);
+                    memset(dst + (size_t)j * ss, 0, (size_t)(ss - r));
+                    if (r) memcpy(dst + (size_t)j * ss + (ss - r), data + pos, (size_t)r);
+                }
+            }
+            memcpy(gtags + i * tw, tags + ix * tw, tw);
+        }
+    }
+};
+
 template <int NL>
 int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
-               const uint8_t *chal_key, size_t key_len, u64 chunks, const uint8_t *vmax_be,
-               size_t vmax_len, const uint8_t *tags, u64 ntags, const uint8_t *data, u64 len,
-               u32 flags, uint8_t *mu_out, uint8_t *sigma_out) {
+               const uint8_t *chal_key, size_t key_len, u64 chunk_begin, u64 chunk_end, u64 chunks,
+               const uint8_t *vmax_be, size_t vmax_len, const uint8_t *tags, u64 ntags,
+               const uint8_t *data, u64 len, u32 flags, uint8_t *mu_out, uint8_t *sigma_out) {
     Limbs p = from_be(p_be, p_len, NL);
     const u64 C = (u64)pi.ss * S;
     const u32 ncols = S + 1;
     // cxx prove (shacham_waters_private.cxx:731-789): a challenge of at least
     // #tags chunks checks every block in order without the index PRF
-    // (check_all, :754-755, 762); both PRFs are the cxx prf; block offsets are
-    // computed in unsigned int (index*chunk_size, :738, 763).
+    // (check_all, :754-755, 762); both PRFs are the cxx prf; sector offsets
+    // are computed in unsigned int (:738, 762-763).
     const bool cxx = flags & HB_PRF_CXX;
     const bool check_all = cxx && chunks >= ntags;
     if (check_all) chunks = ntags;
     if (cxx && (ntags >> 32)) return fail(c, HB_EUNSUPPORTED, "cxx prove: more than 2^32 - 1 tags");
-    if (chunks == 0) {
+    if (chunk_end > chunks) chunk_end = chunks;
+    if (chunk_begin > chunk_end) chunk_begin = chunk_end;
+    const u64 n = chunk_end - chunk_begin;
+    if (n == 0) {
         memset(mu_out, 0, (size_t)S * pi.tw);
         memset(sigma_out, 0, pi.tw);
         return 0;
     }
-    // idx_i = KeyedPRF(key, ntags)(i), v_i = KeyedPRF(key, v_max)(i)   (PySwizzle.py:344-345)
+    if (c->prove_dirty) {
+        // an earlier prove failed between its two launches: its counters
+        // (normally zeroed by the finalizing workgroup) are cleared here
+        HB_CHECK(hipMemsetAsync(c->queue + HB_QSLOT * 2, 0, 2 * HB_QSLOT * sizeof(unsigned long long), c->stream),
+                 "hipMemsetAsync");
+        if (c->ctl.n) HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync");
+        c->prove_dirty = false;
+    }
+    // stage 1: idx_i = KeyedPRF(key, ntags)(i), v_i = KeyedPRF(key, v_max)(i)   (PySwizzle.py:344-345)
+    ProveArgs<NL> PA;
+    memset(&PA, 0, sizeof PA);
     uint8_t nbe[8];
     u64_be(ntags, nbe);
-    HB_CHECK(c->idx.ensure((size_t)chunks * 8), "hipMalloc(idx)");
-    HB_CHECK(c->vals.ensure((size_t)chunks * NL * 4), "hipMalloc(v)");
-    HB_CHECK(c->wts.ensure((size_t)chunks * NL * 4), "hipMalloc(w)");
-    int rc = 0;
-    if (check_all) {
-        std::vector<u64> iota(chunks);
-        for (u64 i = 0; i < chunks; ++i) iota[i] = i;
-        HB_CHECK(hipMemcpyAsync(c->idx.p, iota.data(), (size_t)chunks * 8, hipMemcpyHostToDevice, c->stream), "H2D");
-        HB_CHECK(hipStreamSynchronize(c->stream), "H2D(idx)");
-    } else {
-        // cxx indexer: limit = #tags, a few bytes -> byte-granular CFB-128 (mode 2)
-        rc = run_prf<2>(c, chal_key, key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 2, cxx ? 2 : 0);
-        if (rc) return rc;
-    }
+    int nr = 0, nr2 = 0;
+    if (!make_prf<2>(chal_key, key_len, nbe, 8, PA.pi, nr2) || !make_prf<NL>(chal_key, key_len, vmax_be, vmax_len, PA.pv, nr))
+        return fail(c, HB_EINVAL, "invalid challenge key");
+    make_mod<NL>(p, PA.mod);
+    Limbs r2 = pow2_mod(64u * NL, p);
+    for (int t = 0; t < NL; ++t) PA.r2[t] = r2[t];
+    HB_CHECK(c->idx.ensure((size_t)n * 8), "hipMalloc(idx)");
+    HB_CHECK(c->wts.ensure((size_t)n * NL * 4), "hipMalloc(v)");
+    if (int rc = ensure_ctl(c, ncols)) return rc;
+    PA.i0 = chunk_begin;
+    PA.n = n;
+    PA.ntags = ntags;
+    PA.check_all = check_all ? 1u : 0u;
+    PA.idx = (u64 *)c->idx.p;
+    PA.vm = (u32 *)c->wts.p;
+    PA.t0 = c->t0;
+    PA.queue = c->queue + HB_QSLOT * 2;   // slots 2 (index) and 3 (v), zero between operations
+    PA.flags = flags_word(c);
     const int vnb = (bitlen_be(vmax_be, vmax_len) + 7) / 8;
-    rc = run_prf<NL>(c, chal_key, key_len, vmax_be, vmax_len, nullptr, 0, chunks, (u32 *)c->vals.p, 3,
-                     cxx ? (vnb % 16 ? 2 : 1) : 0);
-    if (rc) return rc;
-    if (cxx && !check_all) {
-        // after 81 rejected tries the cxx prf returns a value >= the limit
-        // (prf.hxx:142); the reference's t.sigma().at(index) then throws
-        std::vector<u64> hidx(chunks);
-        HB_CHECK(hipMemcpyAsync(hidx.data(), c->idx.p, (size_t)chunks * 8, hipMemcpyDeviceToHost, c->stream),
-                 "hipMemcpy(idx)");
-        HB_CHECK(hipStreamSynchronize(c->stream), "prf");
-        for (u64 i = 0; i < chunks; ++i)
-            if (hidx[i] >= ntags) return fail(c, HB_EINVAL, "vector::_M_range_check: challenge index out of range");
-    }
-    rc = run_mont<NL>(c, p, (const u32 *)c->vals.p, (u32 *)c->wts.p, chunks);
-    if (rc) return rc;
+    const int mode_i = cxx ? 2 : 0, mode_v = cxx ? (vnb % 16 ? 2 : 1) : 0;
+    c->last_launches = 0;
+    HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
+    c->prove_dirty = true;
+    HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, mode_i, mode_v, engine_grid(c, n), c->stream), "hb_prove_prf_kernel launch");
+    c->last_launches++;
 
+    // stage 2: mu_j = sum v_i m_{idx_i, j}, sigma = sum v_i tag[idx_i]   (PySwizzle.py:351-368)
     WsumArgs<NL> A;
     memset(&A, 0, sizeof A);
     make_mod<NL>(p, A.mod);
     A.ncols = ncols;
-    A.idx = (const u64 *)c->idx.p;
-    A.w = (const u32 *)c->wts.p;
-    A.nterms = chunks;
     A.C = C;
     A.ss = pi.ss;
     A.S = S;
     A.tw = pi.tw;
     A.wrap32 = cxx ? 1u : 0u;
-    const u32 gx = wsum_grid(chunks);
-    const u32 nparts = gx * 256;
-    HB_CHECK(c->partials.ensure((size_t)ncols * nparts * NL * 4), "hipMalloc(partials)");
-    A.partials = (u32 *)c->partials.p;
-
+    A.ntags = ntags;
+    A.qslots = PA.queue;
+    A.nslots = 2;
     const bool data_dev = flags & HB_DATA_ON_DEVICE, tags_dev = flags & HB_TAGS_ON_DEVICE;
-    int align = 1;
+    int rc = 0;
     if (data_dev && tags_dev) {
         A.mode = 0;
+        A.idx = check_all ? nullptr : (const u64 *)c->idx.p;
+        A.idx_base = chunk_begin;
+        A.w = (const u32 *)c->wts.p;
+        A.nterms = n;
         A.data = data;
         A.len = len;
         A.tags = tags;
-        align = full16(pi, NL, C, data) ? 16 : 1;
+        A.finalize = 1;
+        rc = launch_wsum<NL>(c, A, full16(pi, NL, C, data) ? 16 : 1);
+        if (rc) return rc;
+        c->last_launches++;
     } else {
-        // Gather the challenged blocks (and their tags) on the host -- the
-        // reference's file.seek/read per index (PySwizzle.py:353-355) -- and
-        // ship only those to the GPU.
-        std::vector<u64> hidx(chunks);
-        HB_CHECK(hipMemcpyAsync(hidx.data(), c->idx.p, (size_t)chunks * 8, hipMemcpyDeviceToHost, c->stream),
-                 "hipMemcpy(idx)");
-        HB_CHECK(hipStreamSynchronize(c->stream), "prf");
-        std::vector<uint8_t> gblocks((size_t)(chunks * C)), gtags((size_t)chunks * pi.tw);
-        std::vector<u64> blen(chunks);
+        // Host bytes: the challenged blocks are gathered on the host -- the
+        // reference's seek/read per index -- in batches of <= 256 MiB staged
+        // through the GPU; each batch adds onto the running sums.
+        std::vector<u64> hidx((size_t)n);
+        if (check_all) {
+            for (u64 i = 0; i < n; ++i) hidx[(size_t)i] = chunk_begin + i;
+        } else {
+            HB_CHECK(hipMemcpyAsync(hidx.data(), c->idx.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream),
+                     "hipMemcpy(idx)");
+        }
+        HB_CHECK(hipStreamSynchronize(c->stream), "prove PRFs");
         std::vector<uint8_t> tagbuf;
         if (tags_dev) {   // rare: device tags with host data
             tagbuf.resize((size_t)(ntags * pi.tw));
             HB_CHECK(hipMemcpy(tagbuf.data(), tags, tagbuf.size(), hipMemcpyDeviceToHost), "hipMemcpy(tags)");
         }
         const uint8_t *htags = tags_dev ? tagbuf.data() : tags;
-        std::vector<uint8_t> blkbuf;
-        for (u64 i = 0; i < chunks; ++i) {
-            const u64 ix = hidx[i];
-            if (ix >= ntags) return fail(c, HB_EINVAL, "internal: index out of range");
-            const u64 off = cxx ? (u64)(u32)(ix * C) : ix * C;
-            const u64 n = off >= len ? 0 : (len - off < C ? len - off : C);
-            blen[i] = n;
-            if (n) {
-                if (data_dev) {
-                    HB_CHECK(hipMemcpy(&gblocks[(size_t)(i * C)], data + off, (size_t)n, hipMemcpyDeviceToHost),
-                             "hipMemcpy(block)");
-                } else {
-                    memcpy(&gblocks[(size_t)(i * C)], data + off, (size_t)n);
-                }
-            }
-            memcpy(&gtags[(size_t)i * pi.tw], htags + ix * pi.tw, pi.tw);
+        std::vector<uint8_t> dbuf;
+        if (data_dev) {   // rare: device data with host tags
+            dbuf.resize((size_t)len);
+            HB_CHECK(hipMemcpy(dbuf.data(), data, (size_t)len, hipMemcpyDeviceToHost), "hipMemcpy(data)");
         }
-        HB_CHECK(c->data[0].ensure(gblocks.size()), "hipMalloc");
-        HB_CHECK(c->gtags.ensure(gtags.size()), "hipMalloc");
-        HB_CHECK(c->blen.ensure(blen.size() * 8), "hipMalloc");
-        HB_CHECK(hipMemcpyAsync(c->data[0].p, gblocks.data(), gblocks.size(), hipMemcpyHostToDevice, c->stream), "H2D");
-        HB_CHECK(hipMemcpyAsync(c->gtags.p, gtags.data(), gtags.size(), hipMemcpyHostToDevice, c->stream), "H2D");
-        HB_CHECK(hipMemcpyAsync(c->blen.p, blen.data(), blen.size() * 8, hipMemcpyHostToDevice, c->stream), "H2D");
-        A.mode = 2;
-        A.data = (const unsigned char *)c->data[0].p;
-        A.len = chunks * C;
-        A.tags = (const unsigned char *)c->gtags.p;
-        A.blen = (const u64 *)c->blen.p;
-        // gathered tags are addressed by position i: identity index
-        std::vector<u64> iota(chunks);
-        for (u64 i = 0; i < chunks; ++i) iota[i] = i;
-        HB_CHECK(c->xs.ensure((size_t)chunks * 8), "hipMalloc");
-        HB_CHECK(hipMemcpyAsync(c->xs.p, iota.data(), (size_t)chunks * 8, hipMemcpyHostToDevice, c->stream), "H2D");
-        A.idx = (const u64 *)c->xs.p;
-        align = full16(pi, NL, C, (const uint8_t *)c->data[0].p) ? 16 : 1;
-        HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");
-        std::vector<uint8_t> out((size_t)ncols * pi.tw);
-        rc = finish_sums<NL>(c, p, ncols, nparts, pi.tw, out.data());
-        if (rc) return rc;
-        memcpy(mu_out, out.data(), (size_t)S * pi.tw);
-        memcpy(sigma_out, out.data() + (size_t)S * pi.tw, pi.tw);
-        return 0;
+        // out-of-range indices (cxx prf after 81 tries) read as zero, reported at the end
+        for (u64 i = 0; i < n; ++i)
+            if (hidx[(size_t)i] >= ntags) hidx[(size_t)i] = 0;
+        Gather G{data_dev ? dbuf.data() : data, len, C, pi.ss, S, pi.tw, cxx, htags};
+        const u64 per = (u64)((256ull << 20) / (C + pi.tw)) ? (256ull << 20) / (C + pi.tw) : 1;
+        const u64 bn = n < per ? n : per;
+        HB_CHECK(c->data[0].ensure((size_t)(bn * C)), "hipMalloc(staging)");
+        HB_CHECK(c->gtags.ensure((size_t)(bn * pi.tw)), "hipMalloc(staging)");
+        std::vector<uint8_t> gblocks((size_t)(bn * C)), gtags((size_t)(bn * pi.tw));
+        for (u64 b0 = 0; b0 < n; b0 += bn) {
+            const u64 m = n - b0 < bn ? n - b0 : bn;
+            // previous batch's kernel reads the staging buffers: wait for it
+            if (b0) HB_CHECK(hipStreamSynchronize(c->stream), "prove batch");
+            G.run(&hidx[(size_t)b0], m, gblocks.data(), gtags.data());
+            HB_CHECK(hipMemcpyAsync(c->data[0].p, gblocks.data(), (size_t)(m * C), hipMemcpyHostToDevice, c->stream), "H2D");
+            HB_CHECK(hipMemcpyAsync(c->gtags.p, gtags.data(), (size_t)(m * pi.tw), hipMemcpyHostToDevice, c->stream), "H2D");
+            A.mode = 2;
+            A.w = (const u32 *)c->wts.p + b0 * NL;
+            A.nterms = m;
+            A.data = (const unsigned char *)c->data[0].p;
+            A.len = m * C;
+            A.tags = (const unsigned char *)c->gtags.p;
+            A.accumulate = b0 ? 1u : 0u;
+            A.finalize = b0 + m == n ? 1u : 0u;
+            rc = launch_wsum<NL>(c, A, full16(pi, NL, C, c->data[0].p) ? 16 : 1);
+            if (rc) return rc;
+            c->last_launches++;
+        }
     }
-    HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");
+    HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
     std::vector<uint8_t> out((size_t)ncols * pi.tw);
-    rc = finish_sums<NL>(c, p, ncols, nparts, pi.tw, out.data());
+    rc = finish_sums<NL>(c, ncols, pi.tw, out.data(), cxx && !check_all);
+    c->prove_dirty = false;   // the finalizing launch ran (its status decides rc)
     if (rc) return rc;
+    float ms = 0.f;
+    HB_CHECK(hipEventElapsedTime(&ms, c->k0, c->k1), "hipEventElapsedTime");
+    c->last_ms = ms;
     memcpy(mu_out, out.data(), (size_t)S * pi.tw);
     memcpy(sigma_out, out.data() + (size_t)S * pi.tw, pi.tw);
     return 0;
@@ -600,17 +679,17 @@ int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             HB_CHECK(hipMemcpyAsync(c->idx.p, iota.data(), (size_t)chunks * 8, hipMemcpyHostToDevice, c->stream), "H2D");
             HB_CHECK(hipStreamSynchronize(c->stream), "H2D(idx)");
         } else {
-            rc = run_prf<2>(c, chal_key, chal_key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 2, cxx ? 2 : 0);
+            rc = run_prf<2>(c, chal_key, chal_key_len, nbe, 8, nullptr, 0, chunks, (u32 *)c->idx.p, 8, cxx ? 2 : 0);
             if (rc) return rc;
         }
-        rc = run_prf<NL>(c, chal_key, chal_key_len, vmax_be, vmax_len, nullptr, 0, chunks, raw, 3, vmode);
+        rc = run_prf<NL>(c, chal_key, chal_key_len, vmax_be, vmax_len, nullptr, 0, chunks, raw, 9, vmode);
         if (rc) return rc;
         // f.eval(index.eval(i))   (PySwizzle.py:389)
-        rc = run_prf<NL>(c, f_key, key_len, p_be, p_len, (const u64 *)c->idx.p, 0, chunks, val, 4, pmode);
+        rc = run_prf<NL>(c, f_key, key_len, p_be, p_len, (const u64 *)c->idx.p, 0, chunks, val, 10, pmode);
         if (rc) return rc;
     }
     // alpha.eval(j)   (PySwizzle.py:392)
-    rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, raw + chunks * NL, 5, pmode);
+    rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, raw + chunks * NL, 11, pmode);
     if (rc) return rc;
     rc = run_mont<NL>(c, p, raw, w, nterms);
     if (rc) return rc;
@@ -629,12 +708,12 @@ int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     A.vals = val;
     A.nterms = nterms;
     A.S = S;
-    const u32 gx = wsum_grid(nterms);
-    const u32 nparts = gx * 256;
-    HB_CHECK(c->partials.ensure((size_t)nparts * NL * 4), "hipMalloc(partials)");
-    A.partials = (u32 *)c->partials.p;
-    HB_CHECK(hb_launch_wsum<NL>(A, 1, (int)gx, c->stream), "hb_wsum_kernel launch");
-    return finish_sums<NL>(c, p, 1, nparts, pi.tw, rhs_out);
+    A.finalize = 1;   // no PRF slots to collect (nslots = 0): checked below
+    rc = launch_wsum<NL>(c, A, 1);
+    if (rc) return rc;
+    rc = finish_sums<NL>(c, 1, pi.tw, rhs_out, false);
+    if (rc) return rc;
+    return check_prf_slots(c);
 }
 
 }  // namespace
@@ -643,6 +722,15 @@ int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 extern "C" {
 
 int hb_abi_version(void) { return HB_ABI_VERSION; }
+
+int hb_device_count(int *n) {
+    if (!n) return HB_EINVAL;
+    *n = 0;
+    int d = 0;
+    if (hipGetDeviceCount(&d) != hipSuccess) return HB_EHIP;
+    *n = d;
+    return 0;
+}
 
 int hb_ctx_create(int device, hb_ctx **out) {
     if (!out) return HB_EINVAL;
@@ -697,8 +785,9 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
                       &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
-                      &c->pfx, &c->retry};
+                      &c->pfx, &c->retry, &c->ctl};
     for (DevBuf *b : bufs) b->release();
+    if (c->hres) (void)hipHostFree(c->hres);
     if (c->t0) (void)hipFree(c->t0);
     if (c->queue) (void)hipFree(c->queue);
     if (c->k0) (void)hipEventDestroy(c->k0);
@@ -837,10 +926,11 @@ int hb_encode(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
     }
 }
 
-int hb_prove(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
-             const uint8_t *chal_key, size_t key_len, uint64_t chunks,
-             const uint8_t *vmax_be, size_t vmax_len, const uint8_t *tags, uint64_t ntags,
-             const uint8_t *data, uint64_t len, uint32_t flags, uint8_t *mu_out, uint8_t *sigma_out) {
+int hb_prove_range(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                   const uint8_t *chal_key, size_t key_len, uint64_t chunks,
+                   uint64_t chunk_begin, uint64_t chunk_end,
+                   const uint8_t *vmax_be, size_t vmax_len, const uint8_t *tags, uint64_t ntags,
+                   const uint8_t *data, uint64_t len, uint32_t flags, uint8_t *mu_out, uint8_t *sigma_out) {
     if (!c) return HB_EINVAL;
     PrimeInfo pi;
     if (int rc = parse_prime(c, p_be, p_len, pi)) return rc;
@@ -852,11 +942,19 @@ int hb_prove(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
     if (vbits > 32 * pi.nl) return fail(c, HB_EUNSUPPORTED, "v_max wider than the prime's limb count");
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     switch (pi.nl) {
-    case 8: return prove_impl<8>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
-    case 16: return prove_impl<16>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
-    case 32: return prove_impl<32>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
-    default: return prove_impl<64>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    case 8: return prove_impl<8>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunk_begin, chunk_end, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    case 16: return prove_impl<16>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunk_begin, chunk_end, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    case 32: return prove_impl<32>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunk_begin, chunk_end, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+    default: return prove_impl<64>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunk_begin, chunk_end, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
     }
+}
+
+int hb_prove(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+             const uint8_t *chal_key, size_t key_len, uint64_t chunks,
+             const uint8_t *vmax_be, size_t vmax_len, const uint8_t *tags, uint64_t ntags,
+             const uint8_t *data, uint64_t len, uint32_t flags, uint8_t *mu_out, uint8_t *sigma_out) {
+    return hb_prove_range(c, p_be, p_len, sectors, chal_key, key_len, chunks, 0, UINT64_MAX, vmax_be, vmax_len,
+                          tags, ntags, data, len, flags, mu_out, sigma_out);
 }
 
 static int verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,

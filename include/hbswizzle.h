@@ -61,6 +61,10 @@ typedef struct hb_ctx hb_ctx;
 
 int hb_abi_version(void);
 
+/* Number of visible HIP devices (multi-GPU sharding of encode / prove opens
+ * one context per device; contexts fail on non-gfx950 devices). */
+int hb_device_count(int *n);
+
 /* Open a context on HIP device `device`.  Replaces nothing in the reference
  * (it runs on the host only); the reference's per-call state lives in
  * PySwizzle objects (PySwizzle.py:233-255). */
@@ -143,6 +147,21 @@ int hb_prove(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
              const uint8_t *tags, uint64_t ntags,
              const uint8_t *data, uint64_t len, uint32_t flags,
              uint8_t *mu_out, uint8_t *sigma_out);
+
+/* The part of hb_prove over challenge indices [chunk_begin, chunk_end) of a
+ * `chunks`-index challenge: mu_out / sigma_out receive that range's sums mod p.
+ * The sums of a partition of [0, chunks) add (mod p) to hb_prove's result:
+ * a prove sharded over several GPUs (one context each) is one call per GPU
+ * plus a host-side sum of S + 1 values mod p.  hb_prove is chunk_begin = 0,
+ * chunk_end = UINT64_MAX.  Replaces the same loop as hb_prove
+ * (PySwizzle.py:351-368; cxx shacham_waters_private.cxx:757-788). */
+int hb_prove_range(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t sectors,
+                   const uint8_t *chal_key, size_t key_len, uint64_t chunks,
+                   uint64_t chunk_begin, uint64_t chunk_end,
+                   const uint8_t *vmax_be, size_t vmax_len,
+                   const uint8_t *tags, uint64_t ntags,
+                   const uint8_t *data, uint64_t len, uint32_t flags,
+                   uint8_t *mu_out, uint8_t *sigma_out);
 
 /* Right-hand side of PySwizzle.verify (PySwizzle.py:381-394) for a decrypted
  * state:  rhs = sum_i v_i * F(idx_i) + sum_j alpha(j) * mu_j  mod p.

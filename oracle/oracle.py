@@ -138,7 +138,7 @@ def cxx_prove(p, sectors, chal_key, chunks, v_max, ntags, tag_at, read_at):
     (cxx/shacham_waters_private.cxx:731-789) over cxx_prf_eval: every block in
     order when chunks >= #tags (check_all, :754-755, 762), else
     idx_i = prf(key, #tags)(i) (:743-744, 762); v_i = prf(key, v_max)(i)
-    (:746-748, 767); block offset (unsigned int)(index * chunk_size) (:738, 763);
+    (:746-748, 767); sector offset (unsigned int)(index * chunk_size + j * ss) (:738, 763);
     duplicate indices count again.  tag_at(k) -> int, read_at(off, n) -> the
     file bytes [off, off + n) clipped at EOF (a seek past EOF reads nothing).
     Parity unpinned (Crypto++ absent)."""
@@ -152,9 +152,10 @@ def cxx_prove(p, sectors, chal_key, chunks, v_max, ntags, tag_at, read_at):
     for i in range(n):
         idx = i if check_all else cxx_prf_eval(chal_key, ntags, i)[0]
         v = cxx_prf_eval(chal_key, v_max, i)[0]
-        off = (idx * C) & 0xffffffff
         for j in range(sectors):
-            mu[j] = (mu[j] + v * int.from_bytes(read_at(off + j * ss, ss), "big")) % p
+            # size_t pos = index*chunk_size + j*_sector_size, all unsigned int (:762-763)
+            pos = (idx * C + j * ss) & 0xffffffff
+            mu[j] = (mu[j] + v * int.from_bytes(read_at(pos, ss), "big")) % p
         sigma = (sigma + v * tag_at(idx)) % p
     return mu, sigma
 

@@ -114,13 +114,16 @@ def test_cxx_prove_vs_oracle(nat, oracle, chunks):
         tb.free()
 
 
-def test_cxx_prove_offsets_wrap_at_4gib(nat, oracle):
-    """A 4.5 GiB device-resident file: challenged blocks past 4 GiB are read at
-    (index * chunk_size) mod 2^32, as the reference's unsigned int arithmetic
-    does (shacham_waters_private.cxx:738, 763)."""
-    p, S = P256, 16
+@pytest.mark.parametrize("S", [16, 3])
+def test_cxx_prove_offsets_wrap_at_4gib(nat, oracle, S):
+    """A 4.5 GiB device-resident file: challenged sectors past 4 GiB are read
+    at (index * chunk_size + j * sector_size) mod 2^32, as the reference's
+    unsigned int arithmetic does (shacham_waters_private.cxx:738, 762-763);
+    with S = 3 (96-byte blocks) block starts are not 2^32-periodic."""
+    p = P256
+    C = 32 * S
     L = 9 << 29
-    ntags = L // 512 + 1
+    ntags = L // C + 1
     buf = DevBuf(nat, L)
     tb = DevBuf(nat, ntags * 32)
     try:
@@ -130,7 +133,7 @@ def test_cxx_prove_offsets_wrap_at_4gib(nat, oracle):
         key = hashlib.sha256(b"wrap").digest()
         chunks = 200
         idx = [oracle.cxx_prf_eval(key, ntags, i)[0] for i in range(chunks)]
-        assert sum(k * 512 >= 1 << 32 for k in idx) > 10
+        assert sum(k * C >= 1 << 32 for k in idx) > 10
         got = _cxx_prove_dev(nat, p, S, key, chunks, p, tb.p, ntags, buf.p, L)
         want = _cxx_prove_want(oracle, p, S, key, chunks, p, ntags,
                                lambda k: int.from_bytes(tb.download(32, k * 32), "big"),

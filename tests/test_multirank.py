@@ -78,3 +78,58 @@ def test_shard_plan_covers_file():
         for a, b in zip(plans, plans[1:]):
             assert a["b0"] + a["nblocks"] == b["b0"]
             assert a["byte_off"] + a["byte_len"] == b["byte_off"] or b["byte_len"] == 0
+
+
+def test_multi_device_selection(monkeypatch):
+    """heartbeat_amd.multi: device list resolution and shard counts."""
+    from heartbeat_amd import multi
+    monkeypatch.setenv("HB_DEVICES", "0,0,1")
+    assert multi.devices() == [0, 0, 1]
+    assert multi.devices([3]) == [3]
+    multi.set_devices([2, 5])
+    try:
+        assert multi.devices() == [2, 5]
+    finally:
+        multi.set_devices(None)
+    # small files stay on one device; large ones use every device
+    assert multi.shard_count(8, 10 << 20, multi.MIN_SHARD_BYTES) == 1
+    assert multi.shard_count(8, 3 * multi.MIN_SHARD_BYTES, multi.MIN_SHARD_BYTES) == 3
+    assert multi.shard_count(8, 64 << 30, multi.MIN_SHARD_BYTES) == 8
+    assert multi.shard_count(2, 0, multi.MIN_SHARD_CHUNKS) == 1
+
+
+def test_multi_run_parallel_order_and_errors():
+    from heartbeat_amd import multi
+    assert multi.run_parallel([lambda k=k: k * k for k in range(5)]) == [0, 1, 4, 9, 16]
+
+    def boom():
+        raise ValueError("x")
+    with pytest.raises(ValueError):
+        multi.run_parallel([lambda: 1, boom])
+
+
+def test_prove_partition_sums_mod_p(oracle):
+    """hb_prove_range's contract on the oracle: partial proofs over a partition
+    of the challenge indices add mod p to the whole proof (PySwizzle.py:351-368
+    sums over i)."""
+    import hashlib
+    p = P256
+    S = 3
+    data = b"".join(hashlib.sha256(b"pp%d" % i).digest() for i in range(200))
+    tags = oracle.encode(p, S, b"f" * 32, b"a" * 32, data)
+    key = b"k" * 32
+    mu, sg = oracle.prove(p, S, key, 40, p, tags, data)
+    # the oracle proves whole challenges only; restate the partition on ints
+    from oracle import oracle as O
+    idx = [O.prf_eval(key, len(tags), i) for i in range(40)]
+    v = [O.prf_eval(key, p, i) for i in range(40)]
+    C = 32 * S
+
+    def part(a, b):
+        m = [sum(v[i] * int.from_bytes(data[idx[i] * C + j * 32: idx[i] * C + (j + 1) * 32], "big")
+                 for i in range(a, b)) % p for j in range(S)]
+        return m, sum(v[i] * tags[idx[i]] for i in range(a, b)) % p
+
+    parts = [part(0, 13), part(13, 27), part(27, 40)]
+    assert [sum(x[0][j] for x in parts) % p for j in range(S)] == mu
+    assert sum(x[1] for x in parts) % p == sg
