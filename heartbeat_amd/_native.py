@@ -55,6 +55,7 @@ SIGNATURES = [
                                      _c.c_uint64, _B, _c.c_size_t, _c.c_uint64, _B, _c.c_size_t,
                                      _B, _P]),
     ("hb_aes_cfb8", _c.c_int, [_B, _c.c_size_t, _B, _B, _P, _c.c_size_t, _c.c_int]),
+    ("hb_aes_cfb128", _c.c_int, [_B, _c.c_size_t, _B, _B, _P, _c.c_size_t, _c.c_int]),
     ("hb_last_kernel_ms", _c.c_int, [_P, _c.POINTER(_c.c_double), _c.POINTER(_c.c_uint32)]),
     ("hb_device_malloc", _c.c_int, [_P, _c.c_uint64, _c.POINTER(_P)]),
     ("hb_device_free", _c.c_int, [_P, _P]),
@@ -149,6 +150,18 @@ def be(n, width=None):
 
 def width_of(p):
     return (int(p).bit_length() + 7) // 8
+
+
+def aes_cfb128(key, iv, data, encrypt):
+    """Host AES-CFB128 (cxx State encrypt-and-sign, shacham_waters_private.cxx:169-306)."""
+    key = bytes(key)
+    iv = bytes(iv)
+    data = bytes(data)
+    out = ctypes.create_string_buffer(max(1, len(data)))
+    rc = lib().hb_aes_cfb128(key, len(key), iv, data, out, len(data), 1 if encrypt else 0)
+    if rc != 0:
+        raise HeartbeatError("AES key must be either 16, 24, or 32 bytes long")
+    return out.raw[:len(data)]
 
 
 def aes_cfb8(key, iv, data, encrypt):

@@ -134,4 +134,21 @@ inline void aes_cfb8(const AesKey &k, const uint8_t iv[16], const uint8_t *in, u
     }
 }
 
+// Full-block CFB (CFB-128, Crypto++ CFB_Mode<AES>, a stream mode: no padding,
+// a final partial block uses the first bytes of its keystream block).
+inline void aes_cfb128(const AesKey &k, const uint8_t iv[16], const uint8_t *in, uint8_t *out,
+                       size_t n, bool encrypt) {
+    uint8_t reg[16], o[16];
+    memcpy(reg, iv, 16);
+    for (size_t i = 0; i < n; i += 16) {
+        aes_encrypt_block(k, reg, o);
+        const size_t m = n - i < 16 ? n - i : 16;
+        for (size_t b = 0; b < m; ++b) {
+            const uint8_t x = in[i + b];
+            out[i + b] = (uint8_t)(x ^ o[b]);
+            reg[b] = encrypt ? out[i + b] : x;   // feedback = ciphertext
+        }
+    }
+}
+
 }  // namespace hbhost

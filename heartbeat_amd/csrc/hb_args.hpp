@@ -22,11 +22,18 @@
 
 // An eval whose first try was rejected, left for the retry pass: its block
 // (relative to the launch) and the CFB-8 shift register after that try.
+// With the MFMA MAC (EncodeArgs::mfma) the first pass has already computed
+// the block's sum_j alpha_j m_ij mod p: `part`, so the retry pass only adds F.
 struct HbRetry {
     u64 blk;
     u64 pad_;
     u32 sr[4];
+    u32 part[8];
 };
+
+// MFMA MAC (hb_mfma_block_acc): the 256-bit sector MAC as an int8 matrix
+// product; sectors per block it accepts (column sums stay inside int32)
+#define HB_MFMA_MAX_S 2048u
 
 template <int NL>
 struct EncodeArgs {
@@ -47,6 +54,14 @@ struct EncodeArgs {
     HbRetry *retry;               // retry list (two-pass encode)
     unsigned long long *retry_count;
     u64 retry_cap;
+    // MFMA MAC (256-bit primes, 32-byte aligned sectors): A-operand fragments
+    // of the signed base-256 digits of alpha_j R mod p ([2][S][64 lanes][16 B])
+    // and the constant kz = Q sum_j (alpha_j R mod p) mod p + p 2^268
+    // (Q = 0x8080..80: the sectors enter the product as bytes - 128)
+    u32 mfma;
+    const u32 *afrag;
+    u32 *sink;                    // scratch word (keeps prefetch loads live)
+    u32 kz[2 * NL + 1];
 };
 
 // Prefix image of one PRF key (hb_prefix_kernel).
@@ -66,6 +81,7 @@ struct PrfArgs {
     u32 *out;                     // n * NL little-endian limbs
     const u32 *t0;
     unsigned long long *queue;
+    u64 qchunk;                   // jobs per queue refill
 };
 
 template <int NL>
@@ -92,6 +108,7 @@ struct ProveArgs {
     const u32 *t0;
     unsigned long long *queue;    // 2 slots: index engine, v engine
     unsigned int *flags;          // bit 0: an index >= #tags (cxx prf after 81 tries)
+    u64 qchunk;                   // jobs per queue refill
 };
 
 // Weighted sums  sum_i w_i * value_{col}(i)  mod p  (w_i in Montgomery form);

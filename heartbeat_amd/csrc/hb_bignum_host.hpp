@@ -75,6 +75,51 @@ inline Limbs pow2_mod(unsigned k, const Limbs &p) {
     return x;
 }
 
+// (a + b) mod p for a, b < p (p.size() limbs).
+inline Limbs add_mod(const Limbs &a, const Limbs &b, const Limbs &p) {
+    size_t nl = p.size();
+    Limbs x(nl + 1, 0), pp(p);
+    pp.push_back(0);
+    uint64_t c = 0;
+    for (size_t t = 0; t < nl; ++t) {
+        c += (uint64_t)a[t] + b[t];
+        x[t] = (uint32_t)c;
+        c >>= 32;
+    }
+    x[nl] = (uint32_t)c;
+    if (cmp(x, pp) >= 0) sub_in_place(x, pp);
+    x.resize(nl);
+    return x;
+}
+
+// x mod p for any limb vector x (bitwise long division).
+inline Limbs mod_any(const Limbs &x, const Limbs &p) {
+    size_t nl = p.size();
+    Limbs r(nl, 0);
+    for (size_t t = x.size(); t-- > 0;)
+        for (int b = 31; b >= 0; --b) {
+            r = add_mod(r, r, p);                       // r = 2r mod p
+            if ((x[t] >> b) & 1u) {
+                Limbs one(nl, 0);
+                one[0] = 1;
+                r = add_mod(r, one, p);
+            }
+        }
+    return r;
+}
+
+// a * b mod p (a, b < p), shift-and-add.
+inline Limbs mul_mod(const Limbs &a, const Limbs &b, const Limbs &p) {
+    size_t nl = p.size();
+    Limbs r(nl, 0);
+    for (size_t t = nl; t-- > 0;)
+        for (int k = 31; k >= 0; --k) {
+            r = add_mod(r, r, p);
+            if ((b[t] >> k) & 1u) r = add_mod(r, a, p);
+        }
+    return r;
+}
+
 // -p^-1 mod 2^32 (p odd), Newton iteration.
 inline uint32_t mont_pinv(uint32_t p0) {
     uint32_t inv = 1;

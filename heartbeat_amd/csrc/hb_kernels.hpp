@@ -65,6 +65,7 @@ struct HbPool {
     u64 next, end, njobs;
     unsigned long long *counter;
     bool exhausted;
+    u64 chunk;   // jobs per refill (HB_QUEUE_CHUNK; 64 for small latency-bound launches)
 
     // Lanes in `mask` (wave-uniform ballot) each want one job; returns whether
     // this lane (if `want`) got one, in `job`.
@@ -75,13 +76,13 @@ struct HbPool {
         u64 base2 = 0, got2 = 0;
         if (avail < need && !exhausted) {
             u64 b = 0;
-            if (hb_lane_id() == 0) b = atomicAdd(counter, (unsigned long long)HB_QUEUE_CHUNK);
+            if (hb_lane_id() == 0) b = atomicAdd(counter, (unsigned long long)chunk);
             b = hb_bcast64(b);
             if (b >= njobs) {
                 exhausted = true;
             } else {
                 base2 = b;
-                got2 = njobs - b < (u64)HB_QUEUE_CHUNK ? njobs - b : (u64)HB_QUEUE_CHUNK;
+                got2 = njobs - b < chunk ? njobs - b : chunk;
             }
         }
         bool ok = false;
@@ -130,8 +131,8 @@ __device__ __forceinline__ void hb_job_digest(const H &h, u64 job, u32 dig[8], l
 
 template <int NL, int NR, class H, int MODE = 0>
 __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParams<NL> &P,
-                                          u64 njobs, unsigned long long *queue) {
-    HbPool pool{0, 0, njobs, queue, false};
+                                          u64 njobs, unsigned long long *queue, u64 chunk = HB_QUEUE_CHUNK) {
+    HbPool pool{0, 0, njobs, queue, false, chunk};
     u64 job = 0;
     bool active = pool.take(__ballot(1), true, job);
     u32 dig[8], sr[4] = {0, 0, 0, 0}, out[NL];
@@ -259,13 +260,122 @@ __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prefix_kernel(PrefixArgs A) {
         A.out[i] = (unsigned char)hb_aes_byte0<NR>(L, A.rk, 0u, 0u, 0u, hb_pfx_s3(i));
 }
 
+// ------------------------------------------------------------------ MFMA MAC
+// sum_j (alpha_j R mod p) m_ij for the 64 blocks of a wave (one per lane) on
+// the matrix cores, for 256-bit primes (ss = 32 = 4 NL, aligned sectors).
+// With alpha'_j = sum_d a_jd 256^d in signed digits a_jd in [-128, 127]
+// (33 digits) and the sector bytes entering as u - 128:
+//     sum_j alpha'_j m_ij = Q sum_j alpha'_j + sum_c D_ic 256^c,
+//     D_ic = sum_j sum_b (u_ijb - 128) a_{j, c-31+b},   c < 64
+// (byte b of a sector has weight 256^(31-b)), i.e. for every sector j one
+// v_mfma_i32_32x32x32_i8 per 32 blocks and 32 output columns: A = the digit
+// Toeplitz matrix of sector j (32 columns c x 32 bytes b, host-built
+// fragments), B = the 32 bytes of sector j of 32 blocks (one 16-byte load per
+// lane).  |D_ic| <= S 32 2^14 < 2^31.  Lanes 0-31 feed blocks of lanes 0-31
+// (group 0), lanes 32-63 ... (group 1); lane half h of a 32x32 result holds
+// the 32-bit limbs 2k + h of its column's block (rows 8q + 4h + r: byte r of
+// limb 8t + 2q + h), so one exchange with lane l ^ 32 gives every lane all
+// 16 limbs of its OWN block.  The lane then forms
+//     T = kz + sum_t L_t 2^(32 t)     (kz = Q sum_j alpha'_j mod p + p 2^268 > 0)
+// with T == sum_j alpha'_j m_ij (mod p), 0 < T < 2^544: the Montgomery
+// accumulator of hb_block_tag without F R, off the VALU.
+typedef int32_t hb_i32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t hb_i32x16 __attribute__((ext_vector_type(16)));
+
+template <int NL>
+__device__ __forceinline__ bool hb_block_full(const EncodeArgs<NL> &A, u64 job) {
+    return (job + 1) * A.C <= A.len;
+}
+
+// Wave-uniform call.  Returns whether THIS lane's T is valid (active lane,
+// block entirely inside the data); T has 2NL+1 = 17 limbs.  Group by group:
+// after group g the lanes of half g (which own group g's blocks) receive the
+// other half's limbs and assemble T; peak registers stay at one group's
+// accumulators.  The sector loads of a group go out HB_MFMA_BATCH at a time
+// before their MFMAs (one memory latency per batch, not per sector); the A
+// fragments come from LDS (`afl`, S <= HB_MFMA_LDS_S) or global memory.
+#define HB_MFMA_BATCH 4
+#define HB_MFMA_LDS_S 16
+template <int NL, bool ALDS>
+__device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const hb_i32x4 *afl, u64 job, bool active,
+                                                  u32 T[2 * NL + 1]) {
+    static_assert(NL == 8, "MFMA MAC: 256-bit primes only");
+    const u32 l = hb_lane_id(), h = l >> 5, n = l & 31u;
+    const bool mine = active && hb_block_full(A, job);
+    const u32 S = A.S;
+#pragma unroll
+    for (u32 g = 0; g < 2; ++g) {
+        // the block of column n in group g: lane 32 g + n's
+        const u64 jb = (u64)__shfl((long long)job, (int)(32 * g + n));
+        const bool ok = __shfl((int)mine, (int)(32 * g + n)) != 0;
+        const hb_i32x4 *src = reinterpret_cast<const hb_i32x4 *>(A.data + jb * A.C + 16u * h);
+        hb_i32x16 acc0 = {}, acc1 = {};
+        for (u32 j0 = 0; j0 < S; j0 += HB_MFMA_BATCH) {
+            hb_i32x4 b[HB_MFMA_BATCH];
+#pragma unroll
+            for (int jj = 0; jj < HB_MFMA_BATCH; ++jj)
+                b[jj] = ok && j0 + jj < S ? src[2 * (j0 + jj)] : hb_i32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int jj = 0; jj < HB_MFMA_BATCH; ++jj) {
+                // past the last sector: a zero B (after the -128 shift) against
+                // the last sector's A adds nothing
+                const bool in = j0 + jj < S;
+                const u32 j = in ? j0 + jj : S - 1;
+                const hb_i32x4 bb = in ? b[jj] ^ (int32_t)0x80808080 : hb_i32x4{0, 0, 0, 0};
+                const hb_i32x4 a0 = afl[j * 64 + l], a1 = afl[(S + j) * 64 + l];
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bb, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bb, acc1, 0, 0, 0);
+            }
+        }
+        // limb 8t + 2q + h of column n's block = bytes acc_t[4q .. 4q+3];
+        // k = 4t + q: limb 2k + h here, 2k + (1 - h) in lane l ^ 32
+        long long mine_l[8], other[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            mine_l[q] = (long long)acc0[4 * q] + ((long long)acc0[4 * q + 1] << 8) +
+                        ((long long)acc0[4 * q + 2] << 16) + ((long long)acc0[4 * q + 3] << 24);
+            mine_l[4 + q] = (long long)acc1[4 * q] + ((long long)acc1[4 * q + 1] << 8) +
+                            ((long long)acc1[4 * q + 2] << 16) + ((long long)acc1[4 * q + 3] << 24);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) other[k] = __shfl_xor(mine_l[k], 32);
+        if (h == g) {
+            // T = kz + sum_t L_t 2^(32 t), signed carries
+            long long carry = 0;
+#pragma unroll
+            for (int t = 0; t <= 2 * NL; ++t) {
+                long long x = (long long)A.kz[t] + carry;
+                if (t < 2 * NL) x += (((u32)t & 1u) == h) ? mine_l[t >> 1] : other[t >> 1];
+                T[t] = (u32)x;
+                carry = x >> 32;
+            }
+        }
+    }
+    return mine;
+}
+
+// tag = (T + F R) R^-1 mod p  (T from hb_mfma_block_acc; F < 2^256 at limbs NL..)
+template <int NL>
+__device__ __forceinline__ void hb_finish_T(u32 T[2 * NL + 1], const u32 F[NL], const ModP<NL> &M, u32 out[NL]) {
+    u64 c = 0;
+    for (int t = 0; t < NL; ++t) {
+        c += (u64)T[NL + t] + F[t];
+        T[NL + t] = (u32)c;
+        c >>= 32;
+    }
+    T[2 * NL] += (u32)c;
+    u32 v[NL + 1];
+    hb_redc<NL>(T, M, v);
+    hb_reduce_small<NL>(v, M, out);
+}
+
 // End of one first try for one job slot of every lane (wave-uniform call):
 // accepted blocks are tagged, rejected ones go to the retry list with their
 // shift register.
 template <int NL, int NR, int ALIGN, class H>
 __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const LaneTab &L, H &h, u64 job,
                                                 bool active, u32 ok, u32 sr[4], u32 out[NL], u32 &tries,
-                                                u32 &failed) {
+                                                u32 &failed, u32 *T, bool tmine) {
     tries += active ? 1u : 0u;
     const u64 rej = __ballot(active && !ok);
     if (rej) {
@@ -278,6 +388,23 @@ __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const L
                 HbRetry *e = A.retry + slot;
                 e->blk = job;
                 *reinterpret_cast<uint4 *>(e->sr) = make_uint4(sr[0], sr[1], sr[2], sr[3]);
+                if constexpr (NL == 8) {
+                    if (A.mfma) {
+                        // the retry pass only adds F: leave sum_j alpha_j m_j mod p
+                        u32 part[NL];
+                        if (tmine) {
+                            u32 v[NL + 1];
+                            hb_redc<NL>(T, A.mod, v);
+                            hb_reduce_small<NL>(v, A.mod, part);
+                        } else {
+                            const u32 zero[NL] = {0, 0, 0, 0, 0, 0, 0, 0};
+                            hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, zero,
+                                                    part);
+                        }
+                        *reinterpret_cast<uint4 *>(e->part) = make_uint4(part[0], part[1], part[2], part[3]);
+                        *reinterpret_cast<uint4 *>(e->part + 4) = make_uint4(part[4], part[5], part[6], part[7]);
+                    }
+                }
             } else {
                 // retry list full (never at its sizing, see hb_runtime.cpp):
                 // finish this eval in place
@@ -293,7 +420,15 @@ __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const L
             }
         }
     }
-    if (active && ok) h.accept(job, out);
+    if (active && ok) {
+        if (tmine) {
+            u32 tag[NL];
+            hb_finish_T<NL>(T, out, A.mod, tag);
+            hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, tag);
+        } else {
+            h.accept(job, out);
+        }
+    }
 }
 
 // Blocks per lane per first-pass iteration.  Two independent evals whose AES
@@ -309,17 +444,53 @@ struct HbFirstNJ { static constexpr int v = NL <= 8 ? HB_FIRST_NJ : 1; };
 template <int NL, int NR, int ALIGN>
 __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
     constexpr int NJ = HbFirstNJ<NL>::v;
-    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    // MFMA MAC for 256-bit primes with aligned full-width sectors (A.mfma set by the host)
+    constexpr bool MF = NL == 8 && ALIGN == 16 && NJ == 1;
+    // MF: the T-table image plus the MFMA A fragments (2 x S x 1 KiB, S <= 16):
+    // 160 KiB, still one workgroup per CU
+    constexpr u32 AFW = MF ? 2u * HB_MFMA_LDS_S * 64u * 4u : 0u;
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS + AFW];
+    const bool alds = MF && A.mfma && A.S <= HB_MFMA_LDS_S;
+    if (alds) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(A.afrag);
+        uint4 *dst = reinterpret_cast<uint4 *>(lds + HB_LDS_WORDS);
+        for (u32 k = threadIdx.x; k < 2u * A.S * 64u; k += blockDim.x) dst[k] = src[k];
+    }
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     EncodeHandler<NL, ALIGN> h{A};
-    HbPool pool{0, 0, A.nblocks, A.queue, false};
-    u32 tries = 0, failed = 0;
+    HbPool pool{0, 0, A.nblocks, A.queue, false, HB_QUEUE_CHUNK};
+    u32 tries = 0, failed = 0, sink = 0;
     for (;;) {
         u64 job0 = 0, job1 = 0;
         const bool act0 = pool.take(__ballot(1), true, job0);
         const bool act1 = NJ == 2 ? pool.take(__ballot(1), true, job1) : false;
         if (!__ballot(act0 || act1)) break;
+        u32 T[2 * NL + 1];
+        bool tmine = false;
+#if !defined(HB_MFMA_AFTER_PRF)
+        if constexpr (MF) {
+            if (alds) tmine = hb_mfma_block_acc<NL, true>(A, reinterpret_cast<const hb_i32x4 *>(lds + HB_LDS_WORDS), job0, act0, T);
+            else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, reinterpret_cast<const hb_i32x4 *>(A.afrag), job0, act0, T);
+        }
+#endif
+        // L2 prefetch of the next iteration's blocks (the lanes' next jobs are
+        // pool.next + lane while the current queue chunk lasts): four dword
+        // loads, one per 128-byte line of a 512-byte block, consumed only at
+        // the end of the iteration, so the MFMA phase of the next iteration
+        // finds its sectors in L2 instead of waiting for HBM
+        u32 pf[4] = {0, 0, 0, 0};
+        if constexpr (MF) {
+            const u64 nj = pool.next + hb_lane_id();
+            if (alds && nj < pool.end && hb_block_full(A, nj)) {
+                const u32 *q = reinterpret_cast<const u32 *>(A.data + nj * A.C);
+                const u32 step = (u32)(A.C / 16u);   // four lines per block at C = 512
+                pf[0] = q[0];
+                pf[1] = q[step];
+                pf[2] = q[2 * step];
+                pf[3] = q[3 * step];
+            }
+        }
         u32 out[NJ][NL], sr[NJ][4];
         u32 okm;
         {
@@ -332,10 +503,17 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
             }
             okm = hb_prf_try_n<NL, NR, 1, NJ>(L, A.prf, sr, dig, out);
         }
-        hb_first_finish<NL, NR, ALIGN>(A, L, h, job0, act0, okm & 1u, sr[0], out[0], tries, failed);
+#if defined(HB_MFMA_AFTER_PRF)
+        if constexpr (MF) {
+            if (alds) tmine = hb_mfma_block_acc<NL, true>(A, reinterpret_cast<const hb_i32x4 *>(lds + HB_LDS_WORDS), job0, act0, T);
+            else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, reinterpret_cast<const hb_i32x4 *>(A.afrag), job0, act0, T);
+        }
+#endif
+        hb_first_finish<NL, NR, ALIGN>(A, L, h, job0, act0, okm & 1u, sr[0], out[0], tries, failed, T, tmine);
+        if constexpr (MF) sink ^= pf[0] ^ pf[1] ^ pf[2] ^ pf[3];
         if (NJ == 2)
             hb_first_finish<NL, NR, ALIGN>(A, L, h, job1, act1, (okm >> 1) & 1u, sr[NJ - 1], out[NJ - 1],
-                                           tries, failed);
+                                           tries, failed, T, false);
     }
     for (int off = 32; off > 0; off >>= 1) {
         tries += __shfl_xor(tries, off);
@@ -343,6 +521,7 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
     }
     if (hb_lane_id() == 0 && tries) atomicAdd(A.queue + 1, (unsigned long long)tries);
     if (hb_lane_id() == 0 && failed) atomicAdd(A.queue + 2, (unsigned long long)failed);
+    if (MF && sink == 0x5EEDF00Du && A.sink) *A.sink = sink;   // keeps the prefetches live
 }
 
 template <int NL, int ALIGN>
@@ -356,7 +535,20 @@ struct RetryHandler {
     __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
         const u64 blk = A.retry[job].blk;
         u32 tag[NL];
-        hb_block_tag<NL, ALIGN>(A.data, A.len, blk, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
+        if (NL == 8 && A.mfma) {
+            // the first pass left sum_j alpha_j m_j mod p: tag = (F + part) mod p
+            u32 v[NL + 1];
+            u64 c = 0;
+            for (int t = 0; t < NL; ++t) {
+                c += (u64)F[t] + A.retry[job].part[t < 8 ? t : 0];
+                v[t] = (u32)c;
+                c >>= 32;
+            }
+            v[NL] = (u32)c;
+            hb_reduce_small<NL>(v, A.mod, tag);
+        } else {
+            hb_block_tag<NL, ALIGN>(A.data, A.len, blk, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
+        }
         hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, tag);
     }
 };
@@ -399,7 +591,7 @@ __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prf_kernel(PrfArgs<NL> A) {
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     PrfHandler<NL> h{A};
-    hb_engine<NL, NR, PrfHandler<NL>, MODE>(h, L, A.prf, A.n, A.queue);
+    hb_engine<NL, NR, PrfHandler<NL>, MODE>(h, L, A.prf, A.n, A.queue, A.qchunk);
 }
 
 // ------------------------------------------------------------------ Montgomery
@@ -454,10 +646,10 @@ __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prove_prf_kernel(ProveArgs<NL
     const LaneTab L = hb_lane_tab(lds);
     if (!A.check_all) {
         ProveIdxHandler<NL> hi{A};
-        hb_engine<2, NR, ProveIdxHandler<NL>, MODE_I>(hi, L, A.pi, A.n, A.queue);
+        hb_engine<2, NR, ProveIdxHandler<NL>, MODE_I>(hi, L, A.pi, A.n, A.queue, A.qchunk);
     }
     ProveVHandler<NL> hv{A};
-    hb_engine<NL, NR, ProveVHandler<NL>, MODE_V>(hv, L, A.pv, A.n, A.queue + HB_QSLOT);
+    hb_engine<NL, NR, ProveVHandler<NL>, MODE_V>(hv, L, A.pv, A.n, A.queue + HB_QSLOT, A.qchunk);
 }
 
 // ------------------------------------------------------------------ prove stage 2 / verify: weighted sums
@@ -492,6 +684,25 @@ __device__ __forceinline__ void hb_add_mod(u32 r[NL], const u32 *x, const ModP<N
     for (int t = 0; t < NL; ++t) r[t] = o[t];
 }
 
+// sh[k*(NL+1) ..]: n values of NL+1 limbs (whose total fits NL+1 limbs);
+// leaves their sum in sh[0 .. NL].  Block-wide call.
+template <int NL>
+__device__ __forceinline__ void hb_tree_sum(u32 *sh, u32 n) {
+    for (u32 sft = n / 2; sft > 0; sft >>= 1) {
+        if (threadIdx.x < sft) {
+            u32 *x = sh + threadIdx.x * (NL + 1);
+            const u32 *y = sh + (threadIdx.x + sft) * (NL + 1);
+            u64 c = 0;
+            for (int t = 0; t <= NL; ++t) {
+                c += (u64)x[t] + y[t];
+                x[t] = (u32)c;
+                c >>= 32;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // column col of the weighted sum, term i:  w_i * value_col(i)
 //   mode 0 (prove, device-resident file): col < S -> sector col of block idx_i
 //          (absolute offset idx_i*C + col*ss, unsigned int arithmetic in the
@@ -508,7 +719,7 @@ __device__ __forceinline__ void hb_add_mod(u32 r[NL], const u32 *x, const ModP<N
 // two launches with no memset.
 template <int NL, int ALIGN>
 __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
-    __shared__ u32 sh[HB_WSUM_WG * NL];
+    __shared__ u32 sh[HB_WSUM_WG * (NL + 1)];
     __shared__ unsigned int last;
     const u32 col = blockIdx.y;
     const u64 tid = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -538,19 +749,18 @@ __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
     u32 v[NL + 1], r[NL];
     hb_redc<NL>(acc, A.mod, v);
     hb_reduce_small<NL>(v, A.mod, r);
-    // workgroup tree reduction mod p
-    for (int t = 0; t < NL; ++t) sh[threadIdx.x * NL + t] = r[t];
+    // workgroup tree sum of the residues: plain (NL+1)-limb adds, < 256 p,
+    // one reduction at the end
+    for (int t = 0; t < NL; ++t) sh[threadIdx.x * (NL + 1) + t] = r[t];
+    sh[threadIdx.x * (NL + 1) + NL] = 0;
     __syncthreads();
-    for (u32 sft = blockDim.x / 2; sft > 0; sft >>= 1) {
-        if (threadIdx.x < sft) {
-            for (int t = 0; t < NL; ++t) r[t] = sh[threadIdx.x * NL + t];
-            hb_add_mod<NL>(r, sh + (threadIdx.x + sft) * NL, A.mod);
-            for (int t = 0; t < NL; ++t) sh[threadIdx.x * NL + t] = r[t];
-        }
-        __syncthreads();
-    }
+    hb_tree_sum<NL>(sh, blockDim.x);
     u32 *part = A.partials + ((u64)col * gridDim.x + blockIdx.x) * NL;
-    if (threadIdx.x < NL) part[threadIdx.x] = sh[threadIdx.x];
+    if (threadIdx.x == 0) {
+        for (int t = 0; t <= NL; ++t) v[t] = sh[t];
+        hb_reduce_small<NL>(v, A.mod, r);
+        for (int t = 0; t < NL; ++t) part[t] = r[t];
+    }
     __syncthreads();
     // the last workgroup of this column finishes it (release / acquire at agent scope)
     if (threadIdx.x == 0) {
@@ -559,16 +769,20 @@ __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
     }
     __syncthreads();
     if (!last) return;
+    // the column's gridDim.x (<= blockDim.x) partials, summed in parallel
+    for (int t = 0; t <= NL; ++t) sh[threadIdx.x * (NL + 1) + t] = 0;
+    if (threadIdx.x < gridDim.x) {
+        const u32 *pp = A.partials + ((u64)col * gridDim.x + threadIdx.x) * NL;
+        for (int t = 0; t < NL; ++t)
+            sh[threadIdx.x * (NL + 1) + t] = __hip_atomic_load(pp + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    hb_tree_sum<NL>(sh, blockDim.x);
     if (threadIdx.x == 0) {
         u32 sum[NL];
-        const u32 *o = A.out + (u64)col * NL;
-        for (int t = 0; t < NL; ++t) sum[t] = A.accumulate ? o[t] : 0u;
-        for (u32 b = 0; b < gridDim.x; ++b) {
-            const u32 *pp = A.partials + ((u64)col * gridDim.x + b) * NL;
-            u32 x[NL];
-            for (int t = 0; t < NL; ++t) x[t] = __hip_atomic_load(pp + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hb_add_mod<NL>(sum, x, A.mod);
-        }
+        for (int t = 0; t <= NL; ++t) v[t] = sh[t];
+        hb_reduce_small<NL>(v, A.mod, sum);
+        if (A.accumulate) hb_add_mod<NL>(sum, A.out + (u64)col * NL, A.mod);
         for (int t = 0; t < NL; ++t) A.out[(u64)col * NL + t] = sum[t];
         A.ctl[col] = 0;
         // the last column to finish closes the operation

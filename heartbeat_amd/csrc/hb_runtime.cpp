@@ -67,6 +67,7 @@ struct hb_ctx {
     unsigned long long *queue = nullptr;   // 16 slots of HB_QSLOT counters
     DevBuf alpha_raw, alpha_mont, xs, vals, vals2, wts, idx, partials, sums, data[2], tags, blen, gtags;
     DevBuf pfx, retry;   // two-pass encode: CFB prefix image, retry list
+    DevBuf afrag;        // MFMA MAC: digit fragments of alpha_j R mod p
     DevBuf ctl;          // wsum column counters + flags (zero between operations)
     bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
     u32 *hres = nullptr; // pinned host copy of wsum results (+ status)
@@ -98,7 +99,9 @@ int nl_for_bits(int bits) {
     if (bits <= 256) return 8;
     if (bits <= 512) return 16;
     if (bits <= 1024) return 32;
+#if !defined(HB_NO_NL64)
     if (bits <= 2048) return 64;
+#endif
     return 0;
 }
 
@@ -133,6 +136,22 @@ int engine_grid(hb_ctx *c, u64 njobs) {
     return (int)(g ? g : 1);
 }
 
+// Latency-bound PRF launches (a few thousand evaluations: challenges, alpha,
+// KeyedPRF batches): every CU, and 64-job queue refills so that the jobs
+// spread over many waves instead of queueing behind a few (each eval is a
+// serial CFB chain); large launches keep 256-job refills.
+struct EngineShape {
+    int grid;
+    u64 chunk;
+};
+EngineShape small_engine(hb_ctx *c, u64 njobs) {
+    const u64 waves = (u64)c->num_cus * (HB_ENGINE_WG / 64);
+    if (njobs >= waves * HB_QUEUE_CHUNK) return {engine_grid(c, njobs), (u64)HB_QUEUE_CHUNK};
+    u64 g = (njobs + 63) / 64;   // 64-job chunks: at most one workgroup (CU) each
+    if (g > (u64)c->num_cus) g = (u64)c->num_cus;
+    return {(int)(g ? g : 1), 64};
+}
+
 int check_key(hb_ctx *c, size_t key_len) {
     if (key_len != 16 && key_len != 24 && key_len != 32)
         return fail(c, HB_EINVAL, "AES key must be either 16, 24, or 32 bytes long");
@@ -157,8 +176,10 @@ int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_
     A.t0 = c->t0;
     A.queue = c->queue + HB_QSLOT * queue_slot;
     if (n == 0) return 0;
+    const EngineShape es = small_engine(c, n);
+    A.qchunk = es.chunk;
     HB_CHECK(hipMemsetAsync(A.queue, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
-    HB_CHECK(hb_launch_prf<NL>(A, nr, mode, engine_grid(c, n), c->stream), "hb_prf_kernel launch");
+    HB_CHECK(hb_launch_prf<NL>(A, nr, mode, es.grid, c->stream), "hb_prf_kernel launch");
     return 0;
 }
 
@@ -234,6 +255,58 @@ u64 retry_capacity(const uint8_t *p_be, size_t p_len, u64 nb) {
     return cap >= (double)nb ? nb : (u64)cap;
 }
 
+// Host-built inputs of the MFMA MAC (hb_kernels.hpp, hb_mfma_block_acc) from
+// alpha_j R mod p (c->alpha_mont, on the device): the A-operand fragments of
+// the signed base-256 digit Toeplitz matrices and kz.
+int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17]) {
+    const int NL = 8;
+    std::vector<u32> am((size_t)S * NL);
+    HB_CHECK(hipMemcpyAsync(am.data(), c->alpha_mont.p, am.size() * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
+    HB_CHECK(hipStreamSynchronize(c->stream), "alpha PRF");
+    std::vector<int8_t> frag((size_t)2 * S * 64 * 16);
+    Limbs sum(NL, 0);
+    for (u32 j = 0; j < S; ++j) {
+        const u32 *a = &am[(size_t)j * NL];
+        Limbs aj(a, a + NL);
+        sum = add_mod(sum, aj, p);
+        // balanced base-256 digits: alpha = sum_i d_i 256^i, d_i in [-128, 127], i <= 32
+        int d[33];
+        int carry = 0;
+        for (int i = 0; i < 32; ++i) {
+            int x = (int)((a[i / 4] >> (8 * (i % 4))) & 0xffu) + carry;
+            carry = x >= 128 ? 1 : 0;
+            d[i] = x - 256 * carry;
+        }
+        d[32] = carry;
+        for (int t = 0; t < 2; ++t)
+            for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < 16; ++e) {
+                    const int col = 32 * t + (l & 31), k = 16 * (l >> 5) + e, i = col - 31 + k;
+                    frag[(((size_t)t * S + j) * 64 + l) * 16 + e] = (int8_t)(i >= 0 && i <= 32 ? d[i] : 0);
+                }
+    }
+    // Q = 0x80..80 (32 bytes): sum_j alpha_j u_j = sum_j alpha_j (u_j - Q) + Q sum_j alpha_j
+    Limbs q(NL, 0x80808080u);
+    Limbs k = mul_mod(mod_any(q, p), sum, p);
+    // kz = k + p 2^268 (> every negative sum_c D_c 256^c: |.| < S 2^511 <= 2^522)
+    u64 carry = 0;
+    for (int t = 0; t <= 2 * NL; ++t) {
+        // p << 268: limb t gets bits from p limbs t - 8 (shift 12 within)
+        u64 ps = 0;
+        const int src = t - 8;
+        if (src >= 0 && src < NL) ps |= (u64)p[src] << 12;
+        if (src - 1 >= 0 && src - 1 < NL) ps |= (u64)p[src - 1] >> 20;
+        ps &= 0xffffffffull;
+        carry += ps + (t < NL ? k[t] : 0u);
+        kz[t] = (u32)carry;
+        carry >>= 32;
+    }
+    HB_CHECK(c->afrag.ensure(frag.size()), "hipMalloc(afrag)");
+    HB_CHECK(hipMemcpyAsync(c->afrag.p, frag.data(), frag.size(), hipMemcpyHostToDevice, c->stream), "H2D(afrag)");
+    HB_CHECK(hipStreamSynchronize(c->stream), "H2D(afrag)");
+    return 0;
+}
+
 template <int NL>
 int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
                 const uint8_t *f_key, const uint8_t *a_key, size_t key_len, u64 block_base,
@@ -253,6 +326,18 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 
     EncodeArgs<NL> A;
     memset(&A, 0, sizeof A);
+    if constexpr (NL == 8) {
+        // MFMA MAC tables (hb_mfma_block_acc): 256-bit primes with whole
+        // 32-byte sectors, PySwizzle PRF, two-pass encode
+        if (!cxx && pi.ss == 32 && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
+            !getenv("HB_NO_MFMA")) {
+            rc = mfma_tables(c, p, S, A.kz);
+            if (rc) return rc;
+            A.mfma = 1;
+            A.afrag = (const u32 *)c->afrag.p;
+            A.sink = (u32 *)(c->queue + HB_QSLOT * 15);   // unused queue slot
+        }
+    }
     int nr = 0;
     if (!make_prf<NL>(f_key, key_len, p_be, p_len, A.prf, nr)) return fail(c, HB_EINVAL, "invalid key");
     make_mod<NL>(p, A.mod);
@@ -420,9 +505,11 @@ int ensure_hres(hb_ctx *c, size_t words) {
 }
 
 u32 wsum_grid(u64 nterms) {
-    // >= 8 terms per thread before a second workgroup per column is worth it
-    u64 g = (nterms + 8 * HB_WSUM_WG - 1) / (8 * HB_WSUM_WG);
-    if (g > 128) g = 128;
+    // one term per thread while the challenge is small (latency-bound
+    // gathers), at most HB_WSUM_WG workgroups per column (the last one sums
+    // the partials one per thread)
+    u64 g = (nterms + HB_WSUM_WG - 1) / HB_WSUM_WG;
+    if (g > HB_WSUM_WG) g = HB_WSUM_WG;
     return (u32)(g ? g : 1);
 }
 
@@ -553,7 +640,9 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     c->last_launches = 0;
     HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
     c->prove_dirty = true;
-    HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, mode_i, mode_v, engine_grid(c, n), c->stream), "hb_prove_prf_kernel launch");
+    const EngineShape es = small_engine(c, 2 * n);
+    PA.qchunk = es.chunk;
+    HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, mode_i, mode_v, es.grid, c->stream), "hb_prove_prf_kernel launch");
     c->last_launches++;
 
     // stage 2: mu_j = sum v_i m_{idx_i, j}, sigma = sum v_i tag[idx_i]   (PySwizzle.py:351-368)
@@ -785,7 +874,7 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
                       &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
-                      &c->pfx, &c->retry, &c->ctl};
+                      &c->pfx, &c->retry, &c->ctl, &c->afrag};
     for (DevBuf *b : bufs) b->release();
     if (c->hres) (void)hipHostFree(c->hres);
     if (c->t0) (void)hipFree(c->t0);
@@ -847,7 +936,11 @@ static int prf_eval_common(hb_ctx *c, const uint8_t *key, size_t key_len, const 
     case 8: rc = run_prf<8>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
     case 16: rc = run_prf<16>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
     case 32: rc = run_prf<32>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
+#if !defined(HB_NO_NL64)
     default: rc = run_prf<64>(c, key, key_len, range_be, range_len, xd, 0, n, vd, 6, 0, dd); break;
+#else
+    default: return fail(c, HB_EUNSUPPORTED, "ranges above 1024 bits: not in this build");
+#endif
     }
     if (rc) return rc;
     std::vector<u32> h(n * (size_t)nl);
@@ -893,7 +986,11 @@ int hb_cxx_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t
     case 8: rc = run_prf<8>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
     case 16: rc = run_prf<16>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
     case 32: rc = run_prf<32>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
+#if !defined(HB_NO_NL64)
     default: rc = run_prf<64>(c, key, key_len, limit_be, limit_len, (const u64 *)c->xs.p, 0, n, (u32 *)c->vals.p, 6, mode); break;
+#else
+    default: return fail(c, HB_EUNSUPPORTED, "ranges above 1024 bits: not in this build");
+#endif
     }
     if (rc) return rc;
     std::vector<u32> h(n * (size_t)nlv);
@@ -922,7 +1019,11 @@ int hb_encode(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
     case 8: return encode_impl<8>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
     case 16: return encode_impl<16>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
     case 32: return encode_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
+#if !defined(HB_NO_NL64)
     default: return encode_impl<64>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, block_base, data, len, nblocks, tags, flags, tries_out);
+#else
+    default: return fail(c, HB_EUNSUPPORTED, "primes above 1024 bits: not in this build");
+#endif
     }
 }
 
@@ -945,7 +1046,11 @@ int hb_prove_range(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sector
     case 8: return prove_impl<8>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunk_begin, chunk_end, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
     case 16: return prove_impl<16>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunk_begin, chunk_end, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
     case 32: return prove_impl<32>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunk_begin, chunk_end, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+#if !defined(HB_NO_NL64)
     default: return prove_impl<64>(c, p_be, p_len, pi, sectors, chal_key, key_len, chunk_begin, chunk_end, chunks, vmax_be, vmax_len, tags, ntags, data, len, flags, mu_out, sigma_out);
+#else
+    default: return fail(c, HB_EUNSUPPORTED, "primes above 1024 bits: not in this build");
+#endif
     }
 }
 
@@ -1000,7 +1105,11 @@ static int verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sec
     case 8: return verify_impl<8>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
     case 16: return verify_impl<16>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
     case 32: return verify_impl<32>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
+#if !defined(HB_NO_NL64)
     default: return verify_impl<64>(c, p_be, p_len, pi, sectors, f_key, alpha_key, key_len, state_chunks, chal_key, chal_key_len, chunks, vmax_be, vmax_len, mu, rhs_out, cxx);
+#else
+    default: return fail(c, HB_EUNSUPPORTED, "primes above 1024 bits: not in this build");
+#endif
     }
 }
 
@@ -1011,6 +1120,14 @@ int hb_aes_cfb8(const uint8_t *key, size_t key_len, const uint8_t *iv, const uin
     AesKey k;
     if (!aes_expand(key, key_len, k)) return HB_EINVAL;
     aes_cfb8(k, iv, in, out, n, encrypt != 0);
+    return 0;
+}
+
+int hb_aes_cfb128(const uint8_t *key, size_t key_len, const uint8_t *iv, const uint8_t *in,
+                  uint8_t *out, size_t n, int encrypt) {
+    AesKey k;
+    if (!aes_expand(key, key_len, k)) return HB_EINVAL;
+    aes_cfb128(k, iv, in, out, n, encrypt != 0);
     return 0;
 }
 

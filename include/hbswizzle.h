@@ -191,6 +191,12 @@ int hb_cxx_verify_rhs(hb_ctx *ctx, const uint8_t *p_be, size_t p_len, uint32_t s
 int hb_aes_cfb8(const uint8_t *key, size_t key_len, const uint8_t *iv,
                 const uint8_t *in, uint8_t *out, size_t n, int encrypt);
 
+/* Host AES-CFB128 (full-block feedback, no padding) for the cxx extension's
+ * State encrypt-and-sign (cxx/shacham_waters_private.cxx:169-306, Crypto++
+ * CFB_Mode<AES>): a few dozen bytes per call, not a hot path. */
+int hb_aes_cfb128(const uint8_t *key, size_t key_len, const uint8_t *iv,
+                  const uint8_t *in, uint8_t *out, size_t n, int encrypt);
+
 /* Device timing of the last hb_encode on this context: milliseconds spent in
  * the encode kernel (HIP events on the kernel's stream), and launch count. */
 int hb_last_kernel_ms(const hb_ctx *ctx, double *ms, uint32_t *launches);

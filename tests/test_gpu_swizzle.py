@@ -30,7 +30,7 @@ def test_round_trip(sw, oracle, frac):
     assert len(tag) == len(DATA) // (10 * 128) + 1
     # tags are the cxx encode of the state's keys
     st = sw.State.fromdict(state.todict())
-    st.decrypt(beat.k_enc)
+    st.decrypt(beat.k_enc, beat.k_mac)
     assert tag.sigma == oracle.cxx_encode(P1024, 10, st.f_key, st.alpha_key, DATA)
     chal = beat.gen_challenge(state)
     assert chal.chunks == int(frac * len(tag))
@@ -69,3 +69,32 @@ def test_serialisation(sw):
     assert sw.Swizzle.fromdict(beat.todict()) == beat
     pub = beat.get_public()
     assert pub.public and pub.k_enc == b"\0" * 32 and pub != beat
+
+
+def test_size_bound_and_wire_round_trip(sw):
+    """tests_unit_swpriv.py:189-204: the binary tag is at most
+    0.104 * |file| + 4 bytes (1024-bit prime, 10 sectors); every object
+    survives pickle / todict round trips after a real encode/prove."""
+    import pickle
+    beat = sw.Swizzle(1.0, 10, prime=P1024)
+    data = DATA * 40
+    tag, state = beat.encode(io.BytesIO(data))
+    assert len(tag.__getstate__()) <= len(data) * 0.104 + 4
+    chal = beat.gen_challenge(state)
+    proof = beat.prove(io.BytesIO(data), chal, tag)
+    for obj in (beat, tag, state, chal, proof):
+        assert pickle.loads(pickle.dumps(obj)) == obj
+        assert type(obj).fromdict(obj.todict()) == obj
+    # the client / server exchange through the wire forms
+    tag2 = sw.Tag.fromdict(tag.todict())
+    chal2 = sw.Challenge.fromdict(chal.todict())
+    proof2 = beat.get_public().prove(io.BytesIO(data), chal2, tag2)
+    assert proof2 == proof
+    assert beat.verify(sw.Proof.fromdict(proof2.todict()), chal, sw.State.fromdict(state.todict()))
+    assert beat.verify(proof, chal, "not a state") is None
+
+
+def test_heartbeat_alias_is_swizzle():
+    import heartbeat_amd
+    from heartbeat_amd import Swizzle as m
+    assert heartbeat_amd.Heartbeat is m.Swizzle
