@@ -60,7 +60,6 @@ struct EncodeArgs {
     // (Q = 0x8080..80: the sectors enter the product as bytes - 128)
     u32 mfma;
     const u32 *afrag;
-    u32 *sink;                    // scratch word (keeps prefetch loads live)
     u32 kz[2 * NL + 1];
 };
 

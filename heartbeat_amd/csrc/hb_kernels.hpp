@@ -460,7 +460,7 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
     const LaneTab L = hb_lane_tab(lds);
     EncodeHandler<NL, ALIGN> h{A};
     HbPool pool{0, 0, A.nblocks, A.queue, false, HB_QUEUE_CHUNK};
-    u32 tries = 0, failed = 0, sink = 0;
+    u32 tries = 0, failed = 0;
     for (;;) {
         u64 job0 = 0, job1 = 0;
         const bool act0 = pool.take(__ballot(1), true, job0);
@@ -468,28 +468,9 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
         if (!__ballot(act0 || act1)) break;
         u32 T[2 * NL + 1];
         bool tmine = false;
-#if !defined(HB_MFMA_AFTER_PRF)
         if constexpr (MF) {
             if (alds) tmine = hb_mfma_block_acc<NL, true>(A, reinterpret_cast<const hb_i32x4 *>(lds + HB_LDS_WORDS), job0, act0, T);
             else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, reinterpret_cast<const hb_i32x4 *>(A.afrag), job0, act0, T);
-        }
-#endif
-        // L2 prefetch of the next iteration's blocks (the lanes' next jobs are
-        // pool.next + lane while the current queue chunk lasts): four dword
-        // loads, one per 128-byte line of a 512-byte block, consumed only at
-        // the end of the iteration, so the MFMA phase of the next iteration
-        // finds its sectors in L2 instead of waiting for HBM
-        u32 pf[4] = {0, 0, 0, 0};
-        if constexpr (MF) {
-            const u64 nj = pool.next + hb_lane_id();
-            if (alds && nj < pool.end && hb_block_full(A, nj)) {
-                const u32 *q = reinterpret_cast<const u32 *>(A.data + nj * A.C);
-                const u32 step = (u32)(A.C / 16u);   // four lines per block at C = 512
-                pf[0] = q[0];
-                pf[1] = q[step];
-                pf[2] = q[2 * step];
-                pf[3] = q[3 * step];
-            }
         }
         u32 out[NJ][NL], sr[NJ][4];
         u32 okm;
@@ -503,14 +484,7 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
             }
             okm = hb_prf_try_n<NL, NR, 1, NJ>(L, A.prf, sr, dig, out);
         }
-#if defined(HB_MFMA_AFTER_PRF)
-        if constexpr (MF) {
-            if (alds) tmine = hb_mfma_block_acc<NL, true>(A, reinterpret_cast<const hb_i32x4 *>(lds + HB_LDS_WORDS), job0, act0, T);
-            else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, reinterpret_cast<const hb_i32x4 *>(A.afrag), job0, act0, T);
-        }
-#endif
         hb_first_finish<NL, NR, ALIGN>(A, L, h, job0, act0, okm & 1u, sr[0], out[0], tries, failed, T, tmine);
-        if constexpr (MF) sink ^= pf[0] ^ pf[1] ^ pf[2] ^ pf[3];
         if (NJ == 2)
             hb_first_finish<NL, NR, ALIGN>(A, L, h, job1, act1, (okm >> 1) & 1u, sr[NJ - 1], out[NJ - 1],
                                            tries, failed, T, false);
@@ -521,7 +495,6 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
     }
     if (hb_lane_id() == 0 && tries) atomicAdd(A.queue + 1, (unsigned long long)tries);
     if (hb_lane_id() == 0 && failed) atomicAdd(A.queue + 2, (unsigned long long)failed);
-    if (MF && sink == 0x5EEDF00Du && A.sink) *A.sink = sink;   // keeps the prefetches live
 }
 
 template <int NL, int ALIGN>

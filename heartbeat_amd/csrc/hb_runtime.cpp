@@ -329,13 +329,14 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     if constexpr (NL == 8) {
         // MFMA MAC tables (hb_mfma_block_acc): 256-bit primes with whole
         // 32-byte sectors, PySwizzle PRF, two-pass encode
-        if (!cxx && pi.ss == 32 && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
+        // (below 4 sectors per block the VALU MAC is cheaper than the MFMA
+        // phase's fixed cost: measured 67.2 vs 72.7 GiB/s at configs[1], S = 1)
+        if (!cxx && pi.ss == 32 && S >= 4 && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
             !getenv("HB_NO_MFMA")) {
             rc = mfma_tables(c, p, S, A.kz);
             if (rc) return rc;
             A.mfma = 1;
             A.afrag = (const u32 *)c->afrag.p;
-            A.sink = (u32 *)(c->queue + HB_QSLOT * 15);   // unused queue slot
         }
     }
     int nr = 0;
