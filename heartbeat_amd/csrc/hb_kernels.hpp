@@ -20,10 +20,11 @@
 // until the queue drains.  One try = nb CFB-8 steps = nb AES encryptions of
 // which only byte 0 is used (hb_lane.hpp).
 //
-// The AES T tables live in LDS as a 64 KiB bank-replicated T0/T1 image
-// (hb_lane.hpp, LaneTab): ds_read_b32 lookups are conflict-free for any
-// indices, and the per-CU LDS rate (one wave-wide ds_read_b32 per 2 cycles)
-// is the kernel's binding resource (roofline).
+// The AES T tables live in LDS as a 128 KiB bank-replicated image of the four
+// tables T0..T3 (hb_lane.hpp, LaneTab): ds_read_b32 lookups are conflict-free
+// for any indices.  The per-CU LDS rate (one wave-wide ds_read_b32 per 2
+// cycles) and the VALU issue rate (address v_perm, v_bitop3 XORs, SHA-256, CFB
+// register) bind the encode together (PMC counters).
 #pragma once
 #include <hip/hip_runtime.h>
 #include "hb_args.hpp"

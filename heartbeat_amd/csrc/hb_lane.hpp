@@ -3,15 +3,15 @@
 // Everything a single lane does for one block lives here:
 //   * SHA-256 of the decimal block index          (heartbeat/util.py:91)
 //   * AES-CFB8 keystream with byte-0-only output   (heartbeat/util.py:88-93)
-//     using a bank-replicated T0/T1 LDS image
+//     using a bank-replicated T0..T3 LDS image (128 KiB)
 //   * the rejection test num < R                    (heartbeat/util.py:94)
 //   * the fixed-width Montgomery multiply-accumulate and reduction of
 //     tag = F(i) + sum_j alpha_j m_ij mod p        (PySwizzle.py:297-307)
 //
 // The header compiles as HIP device code (inlined into the kernels of
-// hb_kernels.hip) and as plain C++ (tests/emul), so the lane logic can be
+// hb_kernels.hpp) and as plain C++ (tests/emul), so the lane logic can be
 // checked against the CPU oracle without a GPU.  Wave-level work distribution
-// (job queue, ballots) is in hb_kernels.hip, not here.
+// (job queue, ballots) is in hb_kernels.hpp, not here.
 #pragma once
 #include <stdint.h>
 
