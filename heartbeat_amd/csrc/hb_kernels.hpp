@@ -289,12 +289,16 @@ __device__ __forceinline__ bool hb_block_full(const EncodeArgs<NL> &A, u64 job) 
 }
 
 // Wave-uniform call.  Returns whether THIS lane's T is valid (active lane,
-// block entirely inside the data); T has 2NL+1 = 17 limbs.  Group by group:
-// after group g the lanes of half g (which own group g's blocks) receive the
-// other half's limbs and assemble T; peak registers stay at one group's
-// accumulators.  The sector loads of a group go out HB_MFMA_BATCH at a time
-// before their MFMAs (one memory latency per batch, not per sector); the A
-// fragments come from LDS (`afl`, S <= HB_MFMA_LDS_S) or global memory.
+// block entirely inside the data); T has 2NL+1 = 17 limbs.  Lane half g
+// (lanes 32g .. 32g+31) owns group g's blocks.  After both groups every lane
+// holds, per group, the 64-bit limbs 2k + h (h = its half) of the group's
+// column-n block; one v_permlane32_swap per dword (lanes 32-63 of the first
+// operand <-> lanes 0-31 of the second, with G0 first and G1 second) then
+// leaves every lane with the EVEN limbs of its own block in the first result
+// and the ODD limbs in the second, and T is assembled once, by all lanes.
+// The sector loads of a group go out HB_MFMA_BATCH at a time before their
+// MFMAs (one memory latency per batch, not per sector); the A fragments come
+// from LDS (`afl`, S <= HB_MFMA_LDS_S) or global memory.
 #define HB_MFMA_BATCH 4
 #define HB_MFMA_LDS_S 16
 template <int NL, bool ALDS>
@@ -304,6 +308,7 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
     const u32 l = hb_lane_id(), h = l >> 5, n = l & 31u;
     const bool mine = active && hb_block_full(A, job);
     const u32 S = A.S;
+    long long G[2][8];   // G[g][k]: limb 2k + h of group g's column-n block
 #pragma unroll
     for (u32 g = 0; g < 2; ++g) {
         // the block of column n in group g: lane 32 g + n's
@@ -329,28 +334,31 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
             }
         }
         // limb 8t + 2q + h of column n's block = bytes acc_t[4q .. 4q+3];
-        // k = 4t + q: limb 2k + h here, 2k + (1 - h) in lane l ^ 32
-        long long mine_l[8], other[8];
+        // k = 4t + q: limb 2k + h
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            mine_l[q] = (long long)acc0[4 * q] + ((long long)acc0[4 * q + 1] << 8) +
-                        ((long long)acc0[4 * q + 2] << 16) + ((long long)acc0[4 * q + 3] << 24);
-            mine_l[4 + q] = (long long)acc1[4 * q] + ((long long)acc1[4 * q + 1] << 8) +
-                            ((long long)acc1[4 * q + 2] << 16) + ((long long)acc1[4 * q + 3] << 24);
+            G[g][q] = (long long)acc0[4 * q] + ((long long)acc0[4 * q + 1] << 8) +
+                      ((long long)acc0[4 * q + 2] << 16) + ((long long)acc0[4 * q + 3] << 24);
+            G[g][4 + q] = (long long)acc1[4 * q] + ((long long)acc1[4 * q + 1] << 8) +
+                          ((long long)acc1[4 * q + 2] << 16) + ((long long)acc1[4 * q + 3] << 24);
         }
+    }
+    long long ev[8], od[8];   // limbs 2k and 2k + 1 of this lane's own block
 #pragma unroll
-        for (int k = 0; k < 8; ++k) other[k] = __shfl_xor(mine_l[k], 32);
-        if (h == g) {
-            // T = kz + sum_t L_t 2^(32 t), signed carries
-            long long carry = 0;
+    for (int k = 0; k < 8; ++k) {
+        const auto lo = __builtin_amdgcn_permlane32_swap((int)(u32)G[0][k], (int)(u32)G[1][k], false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap((int)(G[0][k] >> 32), (int)(G[1][k] >> 32), false, false);
+        ev[k] = (long long)(((u64)(u32)hi[0] << 32) | (u32)lo[0]);
+        od[k] = (long long)(((u64)(u32)hi[1] << 32) | (u32)lo[1]);
+    }
+    // T = kz + sum_t L_t 2^(32 t), signed carries
+    long long carry = 0;
 #pragma unroll
-            for (int t = 0; t <= 2 * NL; ++t) {
-                long long x = (long long)A.kz[t] + carry;
-                if (t < 2 * NL) x += (((u32)t & 1u) == h) ? mine_l[t >> 1] : other[t >> 1];
-                T[t] = (u32)x;
-                carry = x >> 32;
-            }
-        }
+    for (int t = 0; t <= 2 * NL; ++t) {
+        long long x = (long long)A.kz[t] + carry;
+        if (t < 2 * NL) x += (t & 1) ? od[t >> 1] : ev[t >> 1];
+        T[t] = (u32)x;
+        carry = x >> 32;
     }
     return mine;
 }
@@ -370,42 +378,33 @@ __device__ __forceinline__ void hb_finish_T(u32 T[2 * NL + 1], const u32 F[NL], 
     hb_reduce_small<NL>(v, M, out);
 }
 
-// End of one first try for one job slot of every lane (wave-uniform call):
-// accepted blocks are tagged, rejected ones go to the retry list with their
-// shift register.
+// End of the first try of every lane's block (wave-uniform call): accepted
+// blocks are tagged, rejected ones go to the retry list with their shift
+// register (and, with the MFMA MAC, with sum_j alpha_j m_j mod p, so that the
+// retry pass only adds F).  With the MFMA MAC both cases are ONE reduction,
+// (T + F' R) R^-1 mod p with F' = F (accepted) or 0 (rejected): with ~14 %
+// rejected first tries nearly every wave has lanes of both kinds, and two
+// divergent reductions would cost both per wave.
 template <int NL, int NR, int ALIGN, class H>
 __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const LaneTab &L, H &h, u64 job,
                                                 bool active, u32 ok, u32 sr[4], u32 out[NL], u32 &tries,
                                                 u32 &failed, u32 *T, bool tmine) {
     tries += active ? 1u : 0u;
-    const u64 rej = __ballot(active && !ok);
+    const bool rejected = active && !ok;
+    const u64 rej = __ballot(rejected);
+    bool listed = false;
+    HbRetry *e = nullptr;
     if (rej) {
         u64 base = 0;
         if (hb_lane_id() == 0) base = atomicAdd(A.retry_count, (unsigned long long)__popcll(rej));
         base = hb_bcast64(base);
-        if (active && !ok) {
+        if (rejected) {
             const u64 slot = base + hb_mbcnt(rej);
             if (slot < A.retry_cap) {
-                HbRetry *e = A.retry + slot;
+                listed = true;
+                e = A.retry + slot;
                 e->blk = job;
                 *reinterpret_cast<uint4 *>(e->sr) = make_uint4(sr[0], sr[1], sr[2], sr[3]);
-                if constexpr (NL == 8) {
-                    if (A.mfma) {
-                        // the retry pass only adds F: leave sum_j alpha_j m_j mod p
-                        u32 part[NL];
-                        if (tmine) {
-                            u32 v[NL + 1];
-                            hb_redc<NL>(T, A.mod, v);
-                            hb_reduce_small<NL>(v, A.mod, part);
-                        } else {
-                            const u32 zero[NL] = {0, 0, 0, 0, 0, 0, 0, 0};
-                            hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, zero,
-                                                    part);
-                        }
-                        *reinterpret_cast<uint4 *>(e->part) = make_uint4(part[0], part[1], part[2], part[3]);
-                        *reinterpret_cast<uint4 *>(e->part + 4) = make_uint4(part[4], part[5], part[6], part[7]);
-                    }
-                }
             } else {
                 // retry list full (never at its sizing, see hb_runtime.cpp):
                 // finish this eval in place
@@ -421,32 +420,44 @@ __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const L
             }
         }
     }
-    if (active && ok) {
-        if (tmine) {
-            u32 tag[NL];
-            hb_finish_T<NL>(T, out, A.mod, tag);
-            hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, tag);
-        } else {
-            h.accept(job, out);
+    const bool done = active && ok;
+#if defined(HB_EXP_NO_FINISH)   // instruction-count experiment only (wrong tags)
+    if (done) hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, T + 3);
+    return;
+#endif
+    if constexpr (NL == 8) {
+        if (A.mfma) {
+            if (tmine && (done || listed)) {
+                u32 F[NL], res[NL];
+                HB_UNROLL
+                for (int t = 0; t < NL; ++t) F[t] = done ? out[t] : 0u;
+                hb_finish_T<NL>(T, F, A.mod, res);
+                if (done) {
+                    hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, res);
+                } else {
+                    *reinterpret_cast<uint4 *>(e->part) = make_uint4(res[0], res[1], res[2], res[3]);
+                    *reinterpret_cast<uint4 *>(e->part + 4) = make_uint4(res[4], res[5], res[6], res[7]);
+                }
+                return;
+            }
+            if (listed) {
+                // a block the MFMA MAC does not cover (the short last block)
+                const u32 zero[NL] = {0, 0, 0, 0, 0, 0, 0, 0};
+                u32 part[NL];
+                hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, zero, part);
+                *reinterpret_cast<uint4 *>(e->part) = make_uint4(part[0], part[1], part[2], part[3]);
+                *reinterpret_cast<uint4 *>(e->part + 4) = make_uint4(part[4], part[5], part[6], part[7]);
+                return;
+            }
         }
     }
+    if (done) h.accept(job, out);
 }
-
-// Blocks per lane per first-pass iteration.  Two independent evals whose AES
-// interleave double the ds_read_b32 in flight per round (+11 % LDS lookup rate
-// in isolation, scripts/ubench_aes.hip), but at 128 VGPRs the 256-bit encode
-// spills and measured 933 vs 967 GiB/s at configs[2]: one by default.
-#ifndef HB_FIRST_NJ
-#define HB_FIRST_NJ 1
-#endif
-template <int NL>
-struct HbFirstNJ { static constexpr int v = NL <= 8 ? HB_FIRST_NJ : 1; };
 
 template <int NL, int NR, int ALIGN>
 __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
-    constexpr int NJ = HbFirstNJ<NL>::v;
     // MFMA MAC for 256-bit primes with aligned full-width sectors (A.mfma set by the host)
-    constexpr bool MF = NL == 8 && ALIGN == 16 && NJ == 1;
+    constexpr bool MF = NL == 8 && ALIGN == 16;
     // MF: the T-table image plus the MFMA A fragments (2 x S x 1 KiB, S <= 16):
     // 160 KiB, still one workgroup per CU
     constexpr u32 AFW = MF ? 2u * HB_MFMA_LDS_S * 64u * 4u : 0u;
@@ -463,32 +474,27 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
     HbPool pool{0, 0, A.nblocks, A.queue, false, HB_QUEUE_CHUNK};
     u32 tries = 0, failed = 0;
     for (;;) {
-        u64 job0 = 0, job1 = 0;
-        const bool act0 = pool.take(__ballot(1), true, job0);
-        const bool act1 = NJ == 2 ? pool.take(__ballot(1), true, job1) : false;
-        if (!__ballot(act0 || act1)) break;
+        u64 job = 0;
+        const bool act = pool.take(__ballot(1), true, job);
+        if (!__ballot(act)) break;
         u32 T[2 * NL + 1];
         bool tmine = false;
+#if defined(HB_EXP_NO_MFMA)   // instruction-count experiment only (wrong tags)
+        for (int t = 0; t <= 2 * NL; ++t) T[t] = (u32)job + t;
+        tmine = act && hb_block_full(A, job);
+        if (0)
+#endif
         if constexpr (MF) {
-            if (alds) tmine = hb_mfma_block_acc<NL, true>(A, reinterpret_cast<const hb_i32x4 *>(lds + HB_LDS_WORDS), job0, act0, T);
-            else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, reinterpret_cast<const hb_i32x4 *>(A.afrag), job0, act0, T);
+            if (alds) tmine = hb_mfma_block_acc<NL, true>(A, reinterpret_cast<const hb_i32x4 *>(lds + HB_LDS_WORDS), job, act, T);
+            else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, reinterpret_cast<const hb_i32x4 *>(A.afrag), job, act, T);
         }
-        u32 out[NJ][NL], sr[NJ][4];
-        u32 okm;
+        u32 out[NL], sr[4], ok;
         {
-            u32 dig[NJ][8];
-            hb_sha256_decimal(A.block_base + job0, dig[0]);
-            hb_prf_prefix<NL>(A.pfx, A.o0, A.prf, dig[0][0], sr[0], out[0]);
-            if (NJ == 2) {
-                hb_sha256_decimal(A.block_base + job1, dig[NJ - 1]);
-                hb_prf_prefix<NL>(A.pfx, A.o0, A.prf, dig[NJ - 1][0], sr[NJ - 1], out[NJ - 1]);
-            }
-            okm = hb_prf_try_n<NL, NR, 1, NJ>(L, A.prf, sr, dig, out);
+            u32 dig[8];
+            hb_sha256_decimal(A.block_base + job, dig);
+            ok = hb_prf_first_try<NL, NR>(L, A.prf, A.pfx, A.o0, sr, dig, out);
         }
-        hb_first_finish<NL, NR, ALIGN>(A, L, h, job0, act0, okm & 1u, sr[0], out[0], tries, failed, T, tmine);
-        if (NJ == 2)
-            hb_first_finish<NL, NR, ALIGN>(A, L, h, job1, act1, (okm >> 1) & 1u, sr[NJ - 1], out[NJ - 1],
-                                           tries, failed, T, false);
+        hb_first_finish<NL, NR, ALIGN>(A, L, h, job, act, ok, sr, out, tries, failed, T, tmine);
     }
     for (int off = 32; off > 0; off >>= 1) {
         tries += __shfl_xor(tries, off);
@@ -618,12 +624,19 @@ __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prove_prf_kernel(ProveArgs<NL
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
-    if (!A.check_all) {
+    // The two PRFs run side by side on disjoint halves of the grid: the
+    // launch lasts as long as its longest rejection chain (a serial CFB
+    // stream), and running the index chain before the v chain in the same
+    // waves would add the two.
+    const bool idx_half = !A.check_all && gridDim.x > 1 && blockIdx.x < gridDim.x / 2;
+    if (!A.check_all && (idx_half || gridDim.x == 1)) {
         ProveIdxHandler<NL> hi{A};
         hb_engine<2, NR, ProveIdxHandler<NL>, MODE_I>(hi, L, A.pi, A.n, A.queue, A.qchunk);
     }
-    ProveVHandler<NL> hv{A};
-    hb_engine<NL, NR, ProveVHandler<NL>, MODE_V>(hv, L, A.pv, A.n, A.queue + HB_QSLOT, A.qchunk);
+    if (!idx_half) {
+        ProveVHandler<NL> hv{A};
+        hb_engine<NL, NR, ProveVHandler<NL>, MODE_V>(hv, L, A.pv, A.n, A.queue + HB_QSLOT, A.qchunk);
+    }
 }
 
 // ------------------------------------------------------------------ prove stage 2 / verify: weighted sums

@@ -174,15 +174,16 @@ HB_HD void hb_sha256_block(u32 W[16], u32 H[8]) {
             w = W[t];
         } else {
             u32 w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
-            u32 s0 = hb_rotr(w15, 7) ^ hb_rotr(w15, 18) ^ (w15 >> 3);
-            u32 s1 = hb_rotr(w2, 17) ^ hb_rotr(w2, 19) ^ (w2 >> 10);
+            u32 s0 = hb_xor3(hb_rotr(w15, 7), hb_rotr(w15, 18), w15 >> 3);
+            u32 s1 = hb_xor3(hb_rotr(w2, 17), hb_rotr(w2, 19), w2 >> 10);
             w = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
             W[t & 15] = w;
         }
-        u32 S1 = hb_rotr(e, 6) ^ hb_rotr(e, 11) ^ hb_rotr(e, 25);
+        // three-input XORs (v_bitop3): the compiler does not fuse rotr ^ rotr ^ rotr
+        u32 S1 = hb_xor3(hb_rotr(e, 6), hb_rotr(e, 11), hb_rotr(e, 25));
         u32 ch = (e & f) ^ (~e & g);
         u32 t1 = h + S1 + ch + K[t] + w;
-        u32 S0 = hb_rotr(a, 2) ^ hb_rotr(a, 13) ^ hb_rotr(a, 22);
+        u32 S0 = hb_xor3(hb_rotr(a, 2), hb_rotr(a, 13), hb_rotr(a, 22));
         u32 mj = (a & b) ^ (a & c) ^ (b & c);
         u32 t2 = S0 + mj;
         h = g; g = f; f = e; e = d + t1;
@@ -195,15 +196,16 @@ HB_HD void hb_sha256_block(u32 W[16], u32 H[8]) {
 // SHA-256 of ASCII decimal(x) (str(x).encode(), util.py:91); one compression
 // since len <= 20 < 56.  Digest as 8 big-endian words.
 HB_HD void hb_sha256_decimal(u64 x, u32 H[8]) {
+#if defined(HB_EXP_NO_SHA)   // instruction-count experiment only (wrong digests)
+    for (int t = 0; t < 8; ++t) H[t] = (u32)x * 2654435761u + (u32)t * 40503u;
+    return;
+#endif
     // Build the message right-to-left: shifting a 24-byte big-endian register
     // right by one byte per digit and inserting the digit at the top leaves
     // the decimal string left-aligned with the 0x80 pad byte right behind it.
     u32 R0 = 0x80000000u, R1 = 0, R2 = 0, R3 = 0, R4 = 0, R5 = 0;
     u32 n = 0;
-    do {
-        u64 q = x / 10u;
-        u32 dgt = (u32)(x - q * 10u);
-        x = q;
+    auto push = [&](u32 dgt) {
         R5 = hb_alignbit(R4, R5, 8);
         R4 = hb_alignbit(R3, R4, 8);
         R3 = hb_alignbit(R2, R3, 8);
@@ -211,7 +213,19 @@ HB_HD void hb_sha256_decimal(u64 x, u32 H[8]) {
         R1 = hb_alignbit(R0, R1, 8);
         R0 = (R0 >> 8) | ((0x30u + dgt) << 24);
         ++n;
-    } while (x != 0);
+    };
+    // 64-bit divisions only while x needs them; the (common) rest in 32 bits
+    while (x >> 32) {
+        const u64 q = x / 10u;
+        push((u32)(x - q * 10u));
+        x = q;
+    }
+    u32 y = (u32)x;
+    do {
+        const u32 q = y / 10u;
+        push(y - q * 10u);
+        y = q;
+    } while (y != 0);
     u32 W[16] = {R0, R1, R2, R3, R4, R5, 0, 0, 0, 0, 0, 0, 0, 0, 0, n * 8u};
     hb_sha256_block(W, H);
 }
@@ -235,6 +249,39 @@ struct PrfParams {
     u32 topmask;
 };
 
+// One CFB-8 step on the shift register s0..s3 (little-endian words of the 16
+// register bytes): AES it, ciphertext byte c = byte 0 of the output ^ the
+// plaintext byte, shift c in at the top.  The plaintext byte is byte 1 of pk
+// (the other bytes of pk are ignored).  The last round is one S-box lookup,
+// S[x] = byte 1 of T0[x]; XORing pk and the last round key's byte (shifted to
+// byte 1) into that word and picking its byte 1 with the same v_perm that
+// shifts s3 makes the step's bookkeeping 1 v_bitop3 + 1 v_perm + 3 v_alignbit.
+template <int NR>
+HB_HD void hb_cfb8_step(const LaneTab &L, const u32 *rk, u32 &s0, u32 &s1, u32 &s2, u32 &s3, u32 pk) {
+    u32 w0 = s0 ^ rk[0], w1 = s1 ^ rk[1], w2 = s2 ^ rk[2], w3 = s3 ^ rk[3];
+    HB_UNROLL
+    for (int r = 1; r <= NR - 2; ++r) hb_aes_round(L, rk + 4 * r, w0, w1, w2, w3);
+    // byte 0 of round NR-1's column 0 (the other bytes of x are not used)
+    const u32 x = hb_xor3(hb_xor3(hb_t<0, 0>(L, w0), hb_t<1, 1>(L, w1), hb_t<2, 2>(L, w2)), hb_t<3, 3>(L, w3),
+                          rk[4 * (NR - 1)]);
+    const u32 u = hb_xor3(hb_t<0, 0>(L, x), pk, rk[4 * NR] << 8);
+    s0 = hb_alignbit(s1, s0, 8);
+    s1 = hb_alignbit(s2, s1, 8);
+    s2 = hb_alignbit(s3, s2, 8);
+    s3 = hb_perm(u, s3, 0x05030201u);   // {u.1, s3.3, s3.2, s3.1}
+}
+
+// Four CFB-8 steps over the big-endian plaintext word d; returns the four
+// ciphertext bytes as a big-endian word (they are s3 afterwards, oldest lowest).
+template <int NR>
+HB_HD u32 hb_cfb8_word(const LaneTab &L, const u32 *rk, u32 &s0, u32 &s1, u32 &s2, u32 &s3, u32 d) {
+    hb_cfb8_step<NR>(L, rk, s0, s1, s2, s3, d >> 16);
+    hb_cfb8_step<NR>(L, rk, s0, s1, s2, s3, d >> 8);
+    hb_cfb8_step<NR>(L, rk, s0, s1, s2, s3, d);
+    hb_cfb8_step<NR>(L, rk, s0, s1, s2, s3, d << 8);
+    return hb_bswap(s3);
+}
+
 // One rejection-sampling try of KeyedPRF.eval: nb CFB-8 steps continuing the
 // stream held in the shift register sr[0..3] (little-endian words of the 16
 // register bytes).  dig: SHA-256 digest (big-endian words) -- the padded
@@ -251,38 +298,31 @@ HB_HD u32 hb_prf_try_from(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], c
     for (int t = 0; t < 8; ++t) dq[t] = t + FIRST < 8 ? dig[t + FIRST] : 0u;
     HB_UNROLL
     for (int t = FIRST; t < NL; ++t) out[t] = 0;
-    u32 m = FIRST ? 0xffu : P.topmask;
     const u32 nw = P.nb >> 2, tail = P.nb & 3u;
     u32 s0 = sr[0], s1 = sr[1], s2 = sr[2], s3 = sr[3];
+    // mask of the try's first output byte (the top byte of the first word)
+    u32 top = FIRST ? 0xffffffffu : (P.topmask << 24) | 0xffffffu;
     HB_NOUNROLL
-    for (u32 wi = FIRST; wi <= nw; ++wi) {
-        const u32 nbytes = wi < nw ? 4u : tail;
-        if (nbytes == 0) break;
-        u32 dword = dq[0];
+    for (u32 wi = FIRST; wi < nw; ++wi) {
+        const u32 word = hb_cfb8_word<NR>(L, P.rk, s0, s1, s2, s3, dq[0]) & top;
+        top = 0xffffffffu;
         HB_UNROLL
         for (int t = 0; t < 7; ++t) dq[t] = dq[t + 1];
         dq[7] = 0;
-        u32 word = 0;
-        for (u32 bi = 0; bi < nbytes; ++bi) {
-            u32 o = hb_aes_byte0<NR>(L, P.rk, s0, s1, s2, s3);
-            u32 c = ((dword >> (24 - 8 * bi)) & 0xffu) ^ o;
-            s0 = hb_alignbit(s1, s0, 8);
-            s1 = hb_alignbit(s2, s1, 8);
-            s2 = hb_alignbit(s3, s2, 8);
-            s3 = (s3 >> 8) | (c << 24);
-            word = (word << 8) | (c & m);
-            m = 0xffu;
-        }
-        if (nbytes == 4) {
-            HB_UNROLL
-            for (int t = NL - 1; t > 0; --t) out[t] = out[t - 1];
-            out[0] = word;
-        } else {
-            const u32 sh = 32 - 8 * nbytes;   // shift out left by 8*nbytes bits
-            HB_UNROLL
-            for (int t = NL - 1; t > 0; --t) out[t] = hb_alignbit(out[t], out[t - 1], sh);
-            out[0] = hb_alignbit(out[0], word << sh, sh);
-        }
+        HB_UNROLL
+        for (int t = NL - 1; t > 0; --t) out[t] = out[t - 1];
+        out[0] = word;
+    }
+    if (tail) {
+        // 1-3 more bytes (nb % 4): plaintext bytes 0..tail-1 of dq[0]
+        const u32 d = dq[0];
+        for (u32 bi = 0; bi < tail; ++bi) hb_cfb8_step<NR>(L, P.rk, s0, s1, s2, s3, d >> (16 - 8 * bi));
+        const u32 sh = 32 - 8 * tail;   // shift out left by 8*tail bits
+        u32 word = hb_bswap(s3) & (0xffffffffu >> sh);
+        if (!FIRST && nw == 0) word &= (P.topmask << (24 - sh)) | (0xffffffu >> sh);
+        HB_UNROLL
+        for (int t = NL - 1; t > 0; --t) out[t] = hb_alignbit(out[t], out[t - 1], sh);
+        out[0] = hb_alignbit(out[0], word << sh, sh);
     }
     sr[0] = s0; sr[1] = s1; sr[2] = s2; sr[3] = s3;
     // out < R  <=>  out - R borrows
@@ -455,77 +495,6 @@ HB_HD void hb_prf_prefix(const unsigned char *pfx, u32 o0, const PrfParams<NL> &
     sr[0] = sr[1] = sr[2] = 0;
     sr[3] = x | (c3 << 24);
     out[0] = ((c0 & P.topmask) << 24) | (c1 << 16) | (c2 << 8) | c3;
-}
-
-// hb_prf_try_from for N independent evals of the same PRF in lockstep (all
-// at the same point of a try): the AES of the N streams are interleaved
-// (hb_aes_byte0_n).  Returns bit n set iff stream n's try was accepted.
-template <int NL, int NR, int FIRST, int N>
-HB_HD u32 hb_prf_try_n(const LaneTab &L, const PrfParams<NL> &P, u32 sr[N][4], const u32 dig[N][8],
-                       u32 out[N][NL]) {
-    u32 dq[N][8];
-    HB_UNROLL
-    for (int n = 0; n < N; ++n) {
-        HB_UNROLL
-        for (int t = 0; t < 8; ++t) dq[n][t] = t + FIRST < 8 ? dig[n][t + FIRST] : 0u;
-        HB_UNROLL
-        for (int t = FIRST; t < NL; ++t) out[n][t] = 0;
-    }
-    u32 m = FIRST ? 0xffu : P.topmask;
-    const u32 nw = P.nb >> 2, tail = P.nb & 3u;
-    HB_NOUNROLL
-    for (u32 wi = FIRST; wi <= nw; ++wi) {
-        const u32 nbytes = wi < nw ? 4u : tail;
-        if (nbytes == 0) break;
-        u32 dword[N], word[N];
-        HB_UNROLL
-        for (int n = 0; n < N; ++n) {
-            dword[n] = dq[n][0];
-            HB_UNROLL
-            for (int t = 0; t < 7; ++t) dq[n][t] = dq[n][t + 1];
-            dq[n][7] = 0;
-            word[n] = 0;
-        }
-        for (u32 bi = 0; bi < nbytes; ++bi) {
-            u32 o[N];
-            hb_aes_byte0_n<NR, N>(L, P.rk, sr, o);
-            HB_UNROLL
-            for (int n = 0; n < N; ++n) {
-                const u32 c = ((dword[n] >> (24 - 8 * bi)) & 0xffu) ^ o[n];
-                sr[n][0] = hb_alignbit(sr[n][1], sr[n][0], 8);
-                sr[n][1] = hb_alignbit(sr[n][2], sr[n][1], 8);
-                sr[n][2] = hb_alignbit(sr[n][3], sr[n][2], 8);
-                sr[n][3] = (sr[n][3] >> 8) | (c << 24);
-                word[n] = (word[n] << 8) | (c & m);
-            }
-            m = 0xffu;
-        }
-        HB_UNROLL
-        for (int n = 0; n < N; ++n) {
-            if (nbytes == 4) {
-                HB_UNROLL
-                for (int t = NL - 1; t > 0; --t) out[n][t] = out[n][t - 1];
-                out[n][0] = word[n];
-            } else {
-                const u32 sh = 32 - 8 * nbytes;
-                HB_UNROLL
-                for (int t = NL - 1; t > 0; --t) out[n][t] = hb_alignbit(out[n][t], out[n][t - 1], sh);
-                out[n][0] = hb_alignbit(out[n][0], word[n] << sh, sh);
-            }
-        }
-    }
-    u32 okm = 0;
-    HB_UNROLL
-    for (int n = 0; n < N; ++n) {
-        u32 borrow = 0;
-        HB_UNROLL
-        for (int t = 0; t < NL; ++t) {
-            u64 d = (u64)out[n][t] - (u64)P.R[t] - (u64)borrow;
-            borrow = (u32)(d >> 63);
-        }
-        okm |= borrow << n;
-    }
-    return okm;
 }
 
 // The first try of a fresh eval through the prefix image (P.nb >= 4).

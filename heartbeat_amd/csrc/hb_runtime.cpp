@@ -643,7 +643,9 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     c->prove_dirty = true;
     const EngineShape es = small_engine(c, 2 * n);
     PA.qchunk = es.chunk;
-    HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, mode_i, mode_v, es.grid, c->stream), "hb_prove_prf_kernel launch");
+    // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
+    const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
+    HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, mode_i, mode_v, pgrid, c->stream), "hb_prove_prf_kernel launch");
     c->last_launches++;
 
     // stage 2: mu_j = sum v_i m_{idx_i, j}, sigma = sum v_i tag[idx_i]   (PySwizzle.py:351-368)

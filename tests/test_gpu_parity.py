@@ -441,3 +441,53 @@ def test_prove_device_resident_vs_oracle(nat, oracle):
     finally:
         buf.free()
         tb.free()
+
+
+def test_device_resident_4_5gib_sampled_vs_oracle(nat, oracle):
+    """PySwizzle mode past 2^32 bytes: a 4.5 GiB + 333-byte device-resident
+    file (ragged tail), S = 16, 256-bit prime.  Tags of the first and last
+    1,000 blocks (tail included) and 10,000 random blocks == the oracle on the
+    same bytes (regenerated on the host from the SplitMix64 stream, with
+    block_base); then a 2,000-index prove over the whole file (challenged
+    offsets past 4 GiB) == the oracle's prove on the downloaded file."""
+    p, S, C, w = P256, 16, 512, 32
+    L = (9 << 29) + 333
+    nb = L // C + 1
+    seed = 2024
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * w)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, seed))
+        fk, ak = hashlib.sha256(b"big-f").digest(), hashlib.sha256(b"big-a").digest()
+        dev_encode(nat, p, S, fk, ak, buf.p, L, nb, tb.p)
+        tags = tb.download()
+        rng = np.random.default_rng(7)
+        runs = [(0, 1000), (nb - 1000, 1000)] + [(int(b), 1) for b in rng.integers(0, nb, 10000)]
+        for b0, n in runs:
+            lo, hi = b0 * C, min((b0 + n) * C, L)
+            data = splitmix_bytes(seed, lo, hi - lo)
+            want = oracle.encode(p, S, fk, ak, data, block_base=b0, nblocks=n)
+            assert split_tags(tags[b0 * w:(b0 + n) * w], w) == want, b0
+        # prove over the whole file: offsets of challenged blocks past 2^32
+        key = hashlib.sha256(b"big-chal").digest()
+        chunks = 2000
+        mu = ctypes.create_string_buffer(w * S)
+        sg = ctypes.create_string_buffer(w)
+        pb = nat.be(p)
+        ctx.check(nat.lib().hb_prove(ctx.h, pb, 32, S, key, 32, chunks, pb, 32, tb.p, nb, buf.p, L, 3,
+                                     mu, sg))
+        host = np.empty(L, dtype=np.uint8)
+        ctx.check(nat.lib().hb_memcpy(ctx.h, host.ctypes.data, buf.p, L, 2))
+        omu = ctypes.create_string_buffer(w * S)
+        osg = ctypes.create_string_buffer(w)
+        rc = oracle.lib().hbo_prove(pb, len(pb), S, key, 32, chunks, pb, len(pb), nb,
+                                    tags, w, host.ctypes.data, L, omu, osg)
+        assert rc == 0
+        assert (mu.raw, sg.raw) == (omu.raw, osg.raw)
+        # at least one challenged block lies past 4 GiB (else the case is vacuous)
+        idx = [oracle.prf_eval(key, nb, i) for i in range(chunks)]
+        assert max(idx) * C > (1 << 32)
+    finally:
+        buf.free()
+        tb.free()
