@@ -138,3 +138,24 @@ struct WsumArgs {
     u32 nslots;
     unsigned int *flags;
 };
+
+// Merkle chunk positions and leaves (heartbeat/Merkle/Merkle.py:481-515),
+// one lane per seed; each seed is its own AES / HMAC key.
+struct MerkleArgs {
+    const unsigned char *seeds;   // n seeds of seed_len bytes (device)
+    u32 seed_len;                 // 16, 24 or 32 (an AES key, Merkle.py:502)
+    u64 n;
+    // offsets pass: KeyedPRF(seed, range).eval(0), range = filesz - chunksz + 1
+    u32 R[2];                     // range, 2 little-endian limbs
+    u32 nb, topmask;
+    u32 dig0[8];                  // SHA-256("0") (util.py:91 of eval(0))
+    u64 *offsets;                 // n chunk offsets
+    // HMAC pass: HMAC-SHA256(seed, data[offsets[i] - rebase[i]...]) over chunksz bytes
+    const unsigned char *data;
+    u64 len;                      // readable bytes at data
+    const u64 *hoff;              // n message offsets into data
+    u64 chunksz;
+    u32 *digests;                 // n * 8 big-endian words
+    unsigned int *flags;          // bit 1: a PRF did not terminate
+    const u32 *t0;
+};

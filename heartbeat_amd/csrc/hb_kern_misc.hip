@@ -1,5 +1,6 @@
-// Non-template kernels and launchers: prefix image, synthetic data, and the
-// 2-limb PRF used for challenge indices.
+// Non-template kernels and launchers: prefix image, Merkle chunk offsets and
+// HMACs, synthetic data, streaming read, and the 2-limb PRF used for
+// challenge indices.
 #include "hb_kernels.hpp"
 
 hipError_t hb_launch_prefix(const PrefixArgs &A, int nr, int grid, hipStream_t s) {
@@ -7,6 +8,66 @@ hipError_t hb_launch_prefix(const PrefixArgs &A, int nr, int grid, hipStream_t s
     if (nr == 14) hipLaunchKernelGGL((hb_prefix_kernel<14>), g, b, 0, s, A);
     else if (nr == 12) hipLaunchKernelGGL((hb_prefix_kernel<12>), g, b, 0, s, A);
     else hipLaunchKernelGGL((hb_prefix_kernel<10>), g, b, 0, s, A);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ Merkle chunks
+// Chunk offsets of MerkleHelper.get_chunk_hash (Merkle.py:497-504): lane i
+// expands seed i into AES round keys (hb_aes_expand_lane) and runs
+// KeyedPRF(seed_i, filesz - chunksz + 1).eval(0) -- all lanes hash the same
+// x = 0 -- trying until accepted.  NR = 10 / 12 / 14 by seed length.
+template <int NR>
+__global__ __launch_bounds__(256) void hb_merkle_offsets_kernel(MerkleArgs A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L = hb_lane_tab(lds);
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    constexpr int NK = NR - 6;
+    u32 key[NK];
+    const unsigned char *sd = A.seeds + i * A.seed_len;
+    for (int t = 0; t < NK; ++t)
+        key[t] = (u32)sd[4 * t] | ((u32)sd[4 * t + 1] << 8) | ((u32)sd[4 * t + 2] << 16) | ((u32)sd[4 * t + 3] << 24);
+    PrfParams<2> P;
+    hb_aes_expand_lane<NR>(L, key, P.rk);
+    P.R[0] = A.R[0];
+    P.R[1] = A.R[1];
+    P.nb = A.nb;
+    P.topmask = A.topmask;
+    u32 sr[4] = {0, 0, 0, 0}, out[2] = {0, 0}, ok = 0;
+    for (u32 t = 0; t < HB_MAX_TRIES && !ok; ++t) ok = hb_prf_try<2, NR>(L, P, sr, A.dig0, out);
+    if (!ok) atomicOr(A.flags, 2u);
+    A.offsets[i] = (u64)out[0] | ((u64)out[1] << 32);
+}
+
+// HMAC-SHA256(seed_i, data[hoff[i] .. hoff[i] + chunksz)), one lane per seed.
+__global__ __launch_bounds__(256) void hb_hmac_kernel(MerkleArgs A) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    u32 kw[16];
+    const unsigned char *sd = A.seeds + i * A.seed_len;
+    for (int t = 0; t < 16; ++t) {
+        u32 w = 0;
+        for (int k = 0; k < 4; ++k) w = (w << 8) | ((u32)(4 * t + k) < A.seed_len ? sd[4 * t + k] : 0u);
+        kw[t] = w;
+    }
+    u32 d[8];
+    hb_hmac_sha256(kw, A.data, A.len, A.hoff[i], A.chunksz, d);
+    for (int t = 0; t < 8; ++t) A.digests[i * 8 + t] = d[t];
+}
+
+hipError_t hb_launch_merkle_offsets(const MerkleArgs &A, int nr, hipStream_t s) {
+    const u64 grid = (A.n + 255) / 256;
+    dim3 g((u32)grid), b(256);
+    if (nr == 14) hipLaunchKernelGGL((hb_merkle_offsets_kernel<14>), g, b, 0, s, A);
+    else if (nr == 12) hipLaunchKernelGGL((hb_merkle_offsets_kernel<12>), g, b, 0, s, A);
+    else hipLaunchKernelGGL((hb_merkle_offsets_kernel<10>), g, b, 0, s, A);
+    return hipGetLastError();
+}
+
+hipError_t hb_launch_hmac(const MerkleArgs &A, hipStream_t s) {
+    const u64 grid = (A.n + 255) / 256;
+    hipLaunchKernelGGL(hb_hmac_kernel, dim3((u32)grid), dim3(256), 0, s, A);
     return hipGetLastError();
 }
 

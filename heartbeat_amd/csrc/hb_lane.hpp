@@ -151,9 +151,9 @@ HB_HD void hb_aes_byte0_n(const LaneTab &L, const u32 *rk, const u32 s[N][4], u3
 // ------------------------------------------------------------------ SHA-256
 HB_HD u32 hb_rotr(u32 x, u32 n) { return hb_alignbit(x, x, n); }
 
-// One SHA-256 compression from the initial state over the padded message
-// block W (16 big-endian words, clobbered).  Digest as 8 big-endian words.
-HB_HD void hb_sha256_block(u32 W[16], u32 H[8]) {
+// One SHA-256 compression of the message block W (16 big-endian words,
+// clobbered) into the chaining state st (8 words).
+HB_HD void hb_sha256_compress(u32 st[8], u32 W[16]) {
     const u32 K[64] = {
         0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
         0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
@@ -165,8 +165,7 @@ HB_HD void hb_sha256_block(u32 W[16], u32 H[8]) {
         0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
         0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
         0xc67178f2u};
-    u32 a = 0x6a09e667u, b = 0xbb67ae85u, c = 0x3c6ef372u, d = 0xa54ff53au;
-    u32 e = 0x510e527fu, f = 0x9b05688cu, g = 0x1f83d9abu, h = 0x5be0cd19u;
+    u32 a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
     HB_UNROLL
     for (int t = 0; t < 64; ++t) {
         u32 w;
@@ -189,8 +188,20 @@ HB_HD void hb_sha256_block(u32 W[16], u32 H[8]) {
         h = g; g = f; f = e; e = d + t1;
         d = c; c = b; b = a; a = t1 + t2;
     }
-    H[0] = a + 0x6a09e667u; H[1] = b + 0xbb67ae85u; H[2] = c + 0x3c6ef372u; H[3] = d + 0xa54ff53au;
-    H[4] = e + 0x510e527fu; H[5] = f + 0x9b05688cu; H[6] = g + 0x1f83d9abu; H[7] = h + 0x5be0cd19u;
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+HB_HD void hb_sha256_init(u32 st[8]) {
+    st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
+    st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
+}
+
+// One SHA-256 compression from the initial state over the padded message
+// block W (16 big-endian words, clobbered).  Digest as 8 big-endian words.
+HB_HD void hb_sha256_block(u32 W[16], u32 H[8]) {
+    hb_sha256_init(H);
+    hb_sha256_compress(H, W);
 }
 
 // SHA-256 of ASCII decimal(x) (str(x).encode(), util.py:91); one compression
@@ -503,6 +514,100 @@ HB_HD u32 hb_prf_first_try(const LaneTab &L, const PrfParams<NL> &P, const unsig
                            u32 sr[4], const u32 dig[8], u32 out[NL]) {
     hb_prf_prefix<NL>(pfx, o0, P, dig[0], sr, out);
     return hb_prf_try_from<NL, NR, 1>(L, P, sr, dig, out);
+}
+
+// ------------------------------------------------------------------ Merkle chunks
+// heartbeat/Merkle/Merkle.py:481-515 (MerkleHelper.get_chunk_hash): the chunk
+// of a seed starts at KeyedPRF(seed, filesz - chunksz + 1).eval(0) and its
+// leaf is HMAC-SHA256(seed, chunk).  Every seed is its own AES key, so a lane
+// expands its key schedule itself (below) instead of taking uniform round keys.
+
+// S-box of each byte of w in place: S[x] is byte 1 of T0[x], i.e. byte k of
+// T_{(k+3)&3}[x].
+HB_HD u32 hb_subword(const LaneTab &L, u32 w) {
+    return (hb_t<0, 3>(L, w) & 0xffu) | (hb_t<1, 0>(L, w) & 0xff00u) | (hb_t<2, 1>(L, w) & 0xff0000u) |
+           (hb_t<3, 2>(L, w) & 0xff000000u);
+}
+
+// FIPS-197 key expansion in the kernels' word order (little-endian column
+// words, as hbhost::aes_expand): key = NK = NR - 6 words, rk = 4 (NR + 1).
+template <int NR>
+HB_HD void hb_aes_expand_lane(const LaneTab &L, const u32 *key, u32 *rk) {
+    constexpr int NK = NR - 6;
+    const u32 rcon[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+    HB_UNROLL
+    for (int i = 0; i < NK; ++i) rk[i] = key[i];
+    HB_UNROLL
+    for (int i = NK; i < 4 * (NR + 1); ++i) {
+        u32 t = rk[i - 1];
+        if (i % NK == 0) t = hb_subword(L, (t >> 8) | (t << 24)) ^ rcon[i / NK - 1];
+        else if (NK > 6 && i % NK == 4) t = hb_subword(L, t);
+        rk[i] = rk[i - NK] ^ t;
+    }
+}
+
+// HMAC-SHA256 (RFC 2104) of msg = data[off .. off + n) under a key of
+// klen <= 64 bytes given as 16 big-endian words kw (zero padded).  len: bytes
+// readable at data (whole-block word loads are used where they stay inside).
+HB_HD void hb_hmac_sha256(const u32 kw[16], const unsigned char *data, u64 len, u64 off, u64 n, u32 out[8]) {
+    u32 st[8], W[16];
+    hb_sha256_init(st);
+    HB_UNROLL
+    for (int t = 0; t < 16; ++t) W[t] = kw[t] ^ 0x36363636u;
+    hb_sha256_compress(st, W);
+    // inner message: (64 + n) bytes hashed so far + padding
+    const u64 total = n + 9;                       // msg, 0x80, 8-byte length
+    const u64 nblk = (total + 63) / 64;
+    const u64 bits = (64 + n) * 8;
+    for (u64 b = 0; b < nblk; ++b) {
+        const u64 p0 = 64 * b;                     // message position of this block
+        const u64 base = off + p0;
+        if (p0 + 64 <= n && (base & ~3ull) + 68 <= len) {
+            // whole block inside the message: 17 aligned dword loads, funnel-shifted
+            const u64 a = base & ~3ull;
+            const u32 sh = 8u * (u32)(base & 3u);
+            const u32 *q = (const u32 *)(data + a);
+            u32 prev = q[0];
+            HB_UNROLL
+            for (int t = 0; t < 16; ++t) {
+                const u32 nx = q[t + 1];
+                W[t] = hb_bswap(sh ? hb_alignbit(nx, prev, sh) : prev);
+                prev = nx;
+            }
+        } else {
+            HB_UNROLL
+            for (int t = 0; t < 16; ++t) {
+                u32 w = 0;
+                for (int k = 0; k < 4; ++k) {
+                    const u64 p = p0 + 4 * (u64)t + (u64)k;
+                    u32 byte = p < n ? data[off + p] : (p == n ? 0x80u : 0u);
+                    w = (w << 8) | byte;
+                }
+                W[t] = w;
+            }
+            if (b == nblk - 1) {
+                W[14] |= (u32)(bits >> 32);
+                W[15] |= (u32)bits;
+            }
+        }
+        hb_sha256_compress(st, W);
+    }
+    u32 inner[8];
+    HB_UNROLL
+    for (int t = 0; t < 8; ++t) inner[t] = st[t];
+    hb_sha256_init(st);
+    HB_UNROLL
+    for (int t = 0; t < 16; ++t) W[t] = kw[t] ^ 0x5c5c5c5cu;
+    hb_sha256_compress(st, W);
+    HB_UNROLL
+    for (int t = 0; t < 8; ++t) W[t] = inner[t];
+    W[8] = 0x80000000u;
+    HB_UNROLL
+    for (int t = 9; t < 15; ++t) W[t] = 0;
+    W[15] = (64 + 32) * 8;
+    hb_sha256_compress(st, W);
+    HB_UNROLL
+    for (int t = 0; t < 8; ++t) out[t] = st[t];
 }
 
 // ------------------------------------------------------------------ mod p

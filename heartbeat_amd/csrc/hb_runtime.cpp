@@ -31,6 +31,8 @@ template <int NL> hipError_t hb_launch_wsum(const WsumArgs<NL> &, int, int, hipS
 template <int NL> hipError_t hb_launch_prove_prf(const ProveArgs<NL> &, int, int, int, int, hipStream_t);
 hipError_t hb_launch_fill(unsigned char *, u64, u64, hipStream_t);
 hipError_t hb_launch_read(const void *, u64, u32 *, int, hipStream_t);
+hipError_t hb_launch_merkle_offsets(const MerkleArgs &, int, hipStream_t);
+hipError_t hb_launch_hmac(const MerkleArgs &, hipStream_t);
 
 namespace {
 
@@ -69,6 +71,7 @@ struct hb_ctx {
     DevBuf pfx, retry;   // two-pass encode: CFB prefix image, retry list
     DevBuf afrag;        // MFMA MAC: digit fragments of alpha_j R mod p
     DevBuf ctl;          // wsum column counters + flags (zero between operations)
+    DevBuf mseeds, moffs, mdig;   // Merkle chunk seeds, offsets, HMAC digests
     bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
     u32 *hres = nullptr; // pinned host copy of wsum results (+ status)
     size_t hres_n = 0;
@@ -1138,6 +1141,87 @@ int hb_last_kernel_ms(const hb_ctx *c, double *ms, uint32_t *launches) {
     if (!c) return HB_EINVAL;
     if (ms) *ms = c->last_ms;
     if (launches) *launches = c->last_launches;
+    return 0;
+}
+
+// ------------------------------------------------------------------ Merkle chunks
+int hb_merkle_offsets(hb_ctx *c, const uint8_t *seeds, size_t seed_len, uint64_t nseeds, uint64_t filesz,
+                      uint64_t chunksz, uint64_t *offsets) {
+    if (!c) return HB_EINVAL;
+    if (int rc = check_key(c, seed_len)) return rc;
+    if (nseeds == 0) return 0;
+    if (!seeds || !offsets) return fail(c, HB_EINVAL, "NULL buffer");
+    // Merkle.py:497-502: a chunk no larger than the file; range filesz - chunksz + 1
+    if (filesz < chunksz) chunksz = filesz;
+    const u64 range = filesz - chunksz + 1;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    MerkleArgs A;
+    memset(&A, 0, sizeof A);
+    A.seed_len = (u32)seed_len;
+    A.n = nseeds;
+    if (range == 0) return fail(c, HB_EUNSUPPORTED, "Merkle chunk range of 2^64");
+    A.R[0] = (u32)range;
+    A.R[1] = (u32)(range >> 32);
+    int bits = 0;
+    for (u64 r = range; r; r >>= 1) ++bits;
+    A.nb = (u32)(bits + 7) / 8;
+    A.topmask = (1u << (bits - 8 * ((int)A.nb - 1))) - 1u;
+    // SHA-256("0"): eval(0) hashes str(0) (util.py:91)
+    static const u32 dig0[8] = {0x5feceb66u, 0xffc86f38u, 0xd952786cu, 0x6d696c79u,
+                                0xc2dbc239u, 0xdd4e91b4u, 0x6729d73au, 0x27fb57e9u};
+    memcpy(A.dig0, dig0, sizeof dig0);
+    HB_CHECK(c->mseeds.ensure((size_t)nseeds * seed_len), "hipMalloc");
+    HB_CHECK(c->moffs.ensure((size_t)nseeds * 8), "hipMalloc");
+    HB_CHECK(hipMemcpyAsync(c->mseeds.p, seeds, (size_t)nseeds * seed_len, hipMemcpyHostToDevice, c->stream), "H2D");
+    A.seeds = (const unsigned char *)c->mseeds.p;
+    A.offsets = (u64 *)c->moffs.p;
+    if (int rc = ensure_ctl(c, 1)) return rc;
+    A.flags = flags_word(c);
+    A.t0 = c->t0;
+    const int nr = seed_len == 16 ? 10 : seed_len == 24 ? 12 : 14;
+    HB_CHECK(hipMemsetAsync(A.flags, 0, 4, c->stream), "hipMemsetAsync");
+    HB_CHECK(hb_launch_merkle_offsets(A, nr, c->stream), "hb_merkle_offsets_kernel launch");
+    u32 fl = 0;
+    HB_CHECK(hipMemcpyAsync(offsets, c->moffs.p, (size_t)nseeds * 8, hipMemcpyDeviceToHost, c->stream), "D2H");
+    HB_CHECK(hipMemcpyAsync(&fl, A.flags, 4, hipMemcpyDeviceToHost, c->stream), "D2H");
+    HB_CHECK(hipMemsetAsync(A.flags, 0, 4, c->stream), "hipMemsetAsync");   // zero between operations
+    HB_CHECK(hipStreamSynchronize(c->stream), "hb_merkle_offsets_kernel");
+    if (fl & 2u) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate");
+    return 0;
+}
+
+int hb_merkle_chunk_hmacs(hb_ctx *c, const uint8_t *seeds, size_t seed_len, uint64_t nseeds,
+                          const uint8_t *data_dev, uint64_t len, const uint64_t *offsets, uint64_t chunk_len,
+                          uint8_t *digests) {
+    if (!c) return HB_EINVAL;
+    if (seed_len == 0 || seed_len > 64) return fail(c, HB_EINVAL, "HMAC keys of 1..64 bytes");
+    if (nseeds == 0) return 0;
+    if (!seeds || !offsets || !digests || (!data_dev && chunk_len)) return fail(c, HB_EINVAL, "NULL buffer");
+    for (u64 i = 0; i < nseeds; ++i)
+        if (offsets[i] > len || len - offsets[i] < chunk_len)
+            return fail(c, HB_EINVAL, "chunk past the end of the data");
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    MerkleArgs A;
+    memset(&A, 0, sizeof A);
+    A.seed_len = (u32)seed_len;
+    A.n = nseeds;
+    HB_CHECK(c->mseeds.ensure((size_t)nseeds * seed_len), "hipMalloc");
+    HB_CHECK(c->moffs.ensure((size_t)nseeds * 8), "hipMalloc");
+    HB_CHECK(c->mdig.ensure((size_t)nseeds * 32), "hipMalloc");
+    HB_CHECK(hipMemcpyAsync(c->mseeds.p, seeds, (size_t)nseeds * seed_len, hipMemcpyHostToDevice, c->stream), "H2D");
+    HB_CHECK(hipMemcpyAsync(c->moffs.p, offsets, (size_t)nseeds * 8, hipMemcpyHostToDevice, c->stream), "H2D");
+    A.seeds = (const unsigned char *)c->mseeds.p;
+    A.hoff = (const u64 *)c->moffs.p;
+    A.data = data_dev;
+    A.len = len;
+    A.chunksz = chunk_len;
+    A.digests = (u32 *)c->mdig.p;
+    HB_CHECK(hb_launch_hmac(A, c->stream), "hb_hmac_kernel launch");
+    std::vector<u32> h((size_t)nseeds * 8);
+    HB_CHECK(hipMemcpyAsync(h.data(), c->mdig.p, h.size() * 4, hipMemcpyDeviceToHost, c->stream), "D2H");
+    HB_CHECK(hipStreamSynchronize(c->stream), "hb_hmac_kernel");
+    for (size_t k = 0; k < h.size(); ++k)
+        for (int b = 0; b < 4; ++b) digests[4 * k + b] = (uint8_t)(h[k] >> (24 - 8 * b));
     return 0;
 }
 

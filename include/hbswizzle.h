@@ -96,6 +96,26 @@ int hb_prf_eval_digests(hb_ctx *ctx, const uint8_t *key, size_t key_len,
                         const uint8_t *range_be, size_t range_len,
                         const uint8_t *digests, size_t n, uint8_t *out);
 
+/* Merkle chunk positions.
+ * Replaces the KeyedPRF call of heartbeat/Merkle/Merkle.py:497-504
+ * (MerkleHelper.get_chunk_hash): with chunk = min(chunksz, filesz),
+ *   offsets[i] = KeyedPRF(seed_i, filesz - chunk + 1).eval(0)
+ * for nseeds seeds of seed_len (16, 24 or 32) bytes each (every seed is its
+ * own AES key).  seeds and offsets are host buffers. */
+int hb_merkle_offsets(hb_ctx *ctx, const uint8_t *seeds, size_t seed_len, uint64_t nseeds,
+                      uint64_t filesz, uint64_t chunksz, uint64_t *offsets);
+
+/* Merkle chunk leaves.
+ * Replaces the HMAC loop of heartbeat/Merkle/Merkle.py:505-515:
+ *   digests[i] = HMAC-SHA256(seed_i, data[offsets[i] : offsets[i] + chunk_len])
+ * over a DEVICE-resident data buffer of len bytes (every chunk must lie
+ * inside it); one GPU lane hashes one chunk (a serial SHA-256 stream).
+ * seed_len: 1..64 bytes.  seeds, offsets (host) and digests (host,
+ * nseeds * 32 bytes). */
+int hb_merkle_chunk_hmacs(hb_ctx *ctx, const uint8_t *seeds, size_t seed_len, uint64_t nseeds,
+                          const uint8_t *data_dev, uint64_t len, const uint64_t *offsets,
+                          uint64_t chunk_len, uint8_t *digests);
+
 /* Swizzle encode of a run of blocks.
  * Replaces heartbeat/PySwizzle/PySwizzle.py:296-309 (the encode loop) and
  * cxx/shacham_waters_private.cxx:672-697.  For k in [0, nblocks):

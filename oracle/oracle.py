@@ -191,3 +191,22 @@ def verify(p, sectors, f_key, alpha_key, state_chunks, chal_key, chunks, v_max, 
     if rc < 0:
         raise ValueError("oracle verify error %d" % rc)
     return rc == 1
+
+
+def merkle_chunk(seed, filesz, chunksz):
+    """(offset, length) of MerkleHelper.get_chunk_hash's chunk
+    (heartbeat/Merkle/Merkle.py:497-504): chunk = min(chunksz, filesz) bytes at
+    KeyedPRF(seed, filesz - chunk + 1).eval(0)."""
+    if filesz < chunksz:
+        chunksz = filesz
+    return prf_eval(seed, filesz - chunksz + 1, 0), chunksz
+
+
+def merkle_chunk_hash(data, seed, filesz=None, chunksz=8192):
+    """MerkleHelper.get_chunk_hash (Merkle.py:480-515) over the bytes `data`:
+    HMAC-SHA256(seed, data[offset : offset + chunk])."""
+    import hashlib
+    import hmac
+    filesz = len(data) if filesz is None else filesz
+    off, n = merkle_chunk(seed, filesz, chunksz)
+    return hmac.new(bytes(seed), bytes(data[off:off + n]), hashlib.sha256).digest()

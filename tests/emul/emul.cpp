@@ -285,3 +285,58 @@ extern "C" int emul_cxx_prf(const uint8_t *key, size_t keylen, const uint8_t *ra
     if (bits <= 1024) return emul_cxx_prf_t<32>(key, keylen, range_be, rlen, x, out_be, lane);
     return -2;
 }
+
+// ------------------------------------------------------------------ Merkle chunks
+// One lane of hb_merkle_offsets_kernel + hb_hmac_kernel: the seed's own key
+// schedule (hb_aes_expand_lane), KeyedPRF(seed, filesz - chunk + 1).eval(0),
+// then HMAC-SHA256(seed, data[off .. off + chunk)).  Returns the PRF tries.
+template <int NR>
+static int merkle_lane(const uint8_t *seed, size_t seed_len, const uint8_t *data, uint64_t len, uint64_t filesz,
+                       uint64_t chunksz, int lane, uint64_t *off_out, uint8_t *digest) {
+    LaneTab L = make_tab(lane);
+    if (filesz < chunksz) chunksz = filesz;
+    const uint64_t range = filesz - chunksz + 1;
+    constexpr int NK = NR - 6;
+    uint32_t key[NK];
+    for (int t = 0; t < NK; ++t)
+        key[t] = (uint32_t)seed[4 * t] | ((uint32_t)seed[4 * t + 1] << 8) | ((uint32_t)seed[4 * t + 2] << 16) |
+                 ((uint32_t)seed[4 * t + 3] << 24);
+    PrfParams<2> P;
+    memset(&P, 0, sizeof P);
+    hb_aes_expand_lane<NR>(L, key, P.rk);
+    P.R[0] = (uint32_t)range;
+    P.R[1] = (uint32_t)(range >> 32);
+    int bits = 0;
+    for (uint64_t r = range; r; r >>= 1) ++bits;
+    P.nb = (uint32_t)(bits + 7) / 8;
+    P.topmask = (1u << (bits - 8 * ((int)P.nb - 1))) - 1u;
+    uint32_t dig[8], sr[4] = {0, 0, 0, 0}, out[2] = {0, 0};
+    hb_sha256_decimal(0, dig);
+    int tries = 0;
+    uint32_t ok = 0;
+    while (!ok && tries < 100000) {
+        ok = hb_prf_try<2, NR>(L, P, sr, dig, out);
+        ++tries;
+    }
+    const uint64_t off = (uint64_t)out[0] | ((uint64_t)out[1] << 32);
+    *off_out = off;
+    uint32_t kw[16];
+    for (int t = 0; t < 16; ++t) {
+        uint32_t w = 0;
+        for (int k = 0; k < 4; ++k) w = (w << 8) | ((size_t)(4 * t + k) < seed_len ? seed[4 * t + k] : 0u);
+        kw[t] = w;
+    }
+    uint32_t d[8];
+    hb_hmac_sha256(kw, data, len, off, chunksz, d);
+    for (int t = 0; t < 8; ++t)
+        for (int b = 0; b < 4; ++b) digest[4 * t + b] = (uint8_t)(d[t] >> (24 - 8 * b));
+    return tries;
+}
+
+extern "C" int emul_merkle(const uint8_t *seed, size_t seed_len, const uint8_t *data, uint64_t len, uint64_t filesz,
+                           uint64_t chunksz, int lane, uint64_t *off_out, uint8_t *digest) {
+    if (seed_len == 16) return merkle_lane<10>(seed, seed_len, data, len, filesz, chunksz, lane, off_out, digest);
+    if (seed_len == 24) return merkle_lane<12>(seed, seed_len, data, len, filesz, chunksz, lane, off_out, digest);
+    if (seed_len == 32) return merkle_lane<14>(seed, seed_len, data, len, filesz, chunksz, lane, off_out, digest);
+    return -1;
+}

@@ -1,6 +1,7 @@
 """The CPU oracle (oracle/swizzle_oracle.c) against golden vectors produced by
 the reference PySwizzle (tests/golden/make_golden.py).  Pins the oracle."""
 import hashlib
+import os
 
 from conftest import fixture_file
 
@@ -137,3 +138,32 @@ def test_pure_python_port_matches_golden(golden_encode):
         assert tags == [int(t, 16) for t in c["tags"]], c["name"]
         n += 1
     assert n > 100
+
+
+def _merkle_file(name):
+    import hashlib
+    from conftest import fixture_file
+    if name in ("test.txt", "test3.txt"):
+        return fixture_file(name)
+    tag, n = {"rand100k": ("merkle-file", 100003), "tiny5": ("merkle-tiny", 5)}[name]
+    out, i = b"", 0
+    while len(out) < n:
+        out += hashlib.sha256(("%s/%d" % (tag, i)).encode()).digest()
+        i += 1
+    return out[:n]
+
+
+def test_oracle_merkle_chunk_hash_vs_reference(oracle):
+    """oracle.merkle_chunk_hash == the reference MerkleHelper.get_chunk_hash
+    (tests/golden/merkle_cases.json, make_golden_merkle.py)."""
+    import json
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "merkle_cases.json")))
+    from heartbeat_amd.Merkle import MerkleHelper
+    ch = g["chain"]
+    assert [x.hex() for x in MerkleHelper.seed_chain(bytes.fromhex(ch["key"]), bytes.fromhex(ch["seed"]),
+                                                     len(ch["seeds"]))] == ch["seeds"]
+    for c in g["cases"]:
+        data = _merkle_file(c["file"])
+        assert hashlib.sha256(data).hexdigest() == g["files"][c["file"]]["sha256"]
+        for sd, leaf in zip(c["seeds"], c["leaves"]):
+            assert oracle.merkle_chunk_hash(data, bytes.fromhex(sd), None, c["chunksz"]).hex() == leaf
