@@ -577,6 +577,32 @@ def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
         ctx.check(L.hb_host_unregister(ctx.h, tags.ctypes.data))
         ctx.check(L.hb_host_unregister(ctx.h, host.ctypes.data))
     out["pinned_tags_equal_pageable"] = ok
+    # the same bytes through the drop-in API (PySwizzle.py:279-314 ->
+    # heartbeat_amd.PySwizzle.encode_file): a BytesIO (its buffer, zero-copy)
+    # and a real file (read-only mmap, page cache warm), default device set
+    import importlib
+    import io
+    import tempfile
+    pys = importlib.import_module("heartbeat_amd.PySwizzle.PySwizzle")
+    p = int.from_bytes(pb, "big")
+    bio = io.BytesIO(host.tobytes())
+    pys.encode_file(p, S, fk, ak, bio)          # warm-up
+    bio.seek(0)
+    t = time.perf_counter()
+    tag, _ = pys.encode_file(p, S, fk, ak, bio)
+    out["api_bytesio_gib_s"] = round(n / GIB / (time.perf_counter() - t), 3)
+    ok = ok and tag._raw[:nb * 32] == ref.tobytes()
+    del bio, tag
+    with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp")) as fh:
+        host.tofile(fh.name)
+        with open(fh.name, "rb") as f:
+            pys.encode_file(p, S, fk, ak, f)
+            f.seek(0)
+            t = time.perf_counter()
+            tag, _ = pys.encode_file(p, S, fk, ak, f)
+            out["api_file_mmap_gib_s"] = round(n / GIB / (time.perf_counter() - t), 3)
+        ok = ok and tag._raw[:nb * 32] == ref.tobytes()
+    out["api_tags_equal"] = ok
     out["unit"] = "GiB/s"
     return out
 

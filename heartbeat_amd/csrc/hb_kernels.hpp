@@ -182,6 +182,176 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
     if (hb_lane_id() == 0 && failed) atomicAdd(queue + 2, (unsigned long long)failed);
 }
 
+// ------------------------------------------------------------------ quad PRF engine
+// Latency-bound launches (a prove's 2 x 10,000 evaluations, verify, alpha,
+// small KeyedPRF batches) last as long as their longest rejection chain: one
+// lane runs nb serial CFB-8 steps per try, 14 dependent T-table rounds each,
+// and a lone wave issues a round's 16 address v_perm + 16 ds_read_b32 + 8
+// XORs back to back.  Here FOUR lanes run one evaluation: lane q = lane & 3
+// holds column word q of the AES state and looks up T0..T3 of ITS column's
+// four bytes; the XOR of a round's output column c = T0(lane c) ^ T1(lane c+1)
+// ^ T2(lane c+2) ^ T3(lane c+3) ^ rk_c is gathered with DPP quad permutations.
+// A round's serial chain drops from ~40 issued instructions to ~12.  Every
+// lane of a quad computes the same keystream byte, ciphertext and output
+// value, so the rejection test and the job queue stay quad-uniform.
+#define HB_QP(a, b, c, d) ((a) | ((b) << 2) | ((c) << 4) | ((d) << 6))
+
+template <int CTRL>
+__device__ __forceinline__ u32 hb_qdpp(u32 x) {
+    return (u32)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ u64 hb_qbcast64(u64 v) {   // lane q = 0's value to its quad
+    const u32 lo = hb_qdpp<HB_QP(0, 0, 0, 0)>((u32)v), hi = hb_qdpp<HB_QP(0, 0, 0, 0)>((u32)(v >> 32));
+    return ((u64)hi << 32) | lo;
+}
+
+struct QuadLane {
+    LaneTab L;
+    u32 lbq;       // lane base of T_q
+    u32 selq;      // v_perm selector: address of T_q[byte q of x]
+    u32 sels;      // CFB shift: {next.0 | u.1, s.3, s.2, s.1}
+    bool q3;       // the lane holding register bytes 12..15
+};
+
+__device__ __forceinline__ QuadLane hb_quad_lane(const LaneTab &L) {
+    const u32 q = hb_lane_id() & 3u;
+    QuadLane Q;
+    Q.L = L;
+    Q.lbq = q == 0 ? L.lb[0] : q == 1 ? L.lb[1] : q == 2 ? L.lb[2] : L.lb[3];
+    Q.selq = 0x0c020000u | ((4u + q) << 8);
+    Q.q3 = q == 3;
+    Q.sels = Q.q3 ? 0x05030201u : 0x04030201u;
+    return Q;
+}
+
+// One T-table round on the quad's column words (w = column q).
+__device__ __forceinline__ u32 hb_quad_round(const LaneTab &L, u32 w, u32 rk) {
+    const u32 a = hb_t<0, 0>(L, w), b = hb_t<1, 1>(L, w), c = hb_t<2, 2>(L, w), d = hb_t<3, 3>(L, w);
+    const u32 x = hb_xor3(a, rk, hb_qdpp<HB_QP(1, 2, 3, 0)>(b));
+    return hb_xor3(x, hb_qdpp<HB_QP(2, 3, 0, 1)>(c), hb_qdpp<HB_QP(3, 0, 1, 2)>(d));
+}
+
+// hb_cfb8_step for a quad: s = register column q, rkq[r] = rk[4r + q].
+template <int NR>
+__device__ __forceinline__ void hb_quad_cfb8_step(const QuadLane &Q, const u32 *rkq, const u32 *rk, u32 &s, u32 pk) {
+    u32 w = s ^ rkq[0];
+    HB_UNROLL
+    for (int r = 1; r <= NR - 2; ++r) w = hb_quad_round(Q.L, w, rkq[r]);
+    // byte 0 of round NR-1's column 0: lane q contributes T_q[byte q of column q]
+    u32 x = hb_tab_ld(Q.L.tab, hb_perm(w, Q.lbq, Q.selq));
+    x ^= hb_qdpp<HB_QP(1, 0, 3, 2)>(x);
+    x = hb_xor3(x, hb_qdpp<HB_QP(2, 3, 0, 1)>(x), rk[4 * (NR - 1)]);
+    const u32 u = hb_xor3(hb_t<0, 0>(Q.L, x), pk, rk[4 * NR] << 8);   // byte 1: the ciphertext byte
+    const u32 nx = hb_qdpp<HB_QP(1, 2, 3, 0)>(s);
+    s = hb_perm(Q.q3 ? u : nx, s, Q.sels);
+}
+
+// The newest four ciphertext bytes (register bytes 12..15, lane 3) as a
+// big-endian word, on every lane of the quad.
+__device__ __forceinline__ u32 hb_quad_s3_be(u32 s) { return hb_bswap(hb_qdpp<HB_QP(3, 3, 3, 3)>(s)); }
+
+// hb_prf_try (FIRST = 0) for a quad.
+template <int NL, int NR>
+__device__ __forceinline__ u32 hb_quad_prf_try(const QuadLane &Q, const u32 *rkq, const PrfParams<NL> &P, u32 &s,
+                                               const u32 dig[8], u32 out[NL]) {
+    u32 dq[8];
+    HB_UNROLL
+    for (int t = 0; t < 8; ++t) dq[t] = dig[t];
+    HB_UNROLL
+    for (int t = 0; t < NL; ++t) out[t] = 0;
+    const u32 nw = P.nb >> 2, tail = P.nb & 3u;
+    u32 top = (P.topmask << 24) | 0xffffffu;
+    HB_NOUNROLL
+    for (u32 wi = 0; wi < nw; ++wi) {
+        const u32 d = dq[0];
+        hb_quad_cfb8_step<NR>(Q, rkq, P.rk, s, d >> 16);
+        hb_quad_cfb8_step<NR>(Q, rkq, P.rk, s, d >> 8);
+        hb_quad_cfb8_step<NR>(Q, rkq, P.rk, s, d);
+        hb_quad_cfb8_step<NR>(Q, rkq, P.rk, s, d << 8);
+        const u32 word = hb_quad_s3_be(s) & top;
+        top = 0xffffffffu;
+        HB_UNROLL
+        for (int t = 0; t < 7; ++t) dq[t] = dq[t + 1];
+        dq[7] = 0;
+        HB_UNROLL
+        for (int t = NL - 1; t > 0; --t) out[t] = out[t - 1];
+        out[0] = word;
+    }
+    if (tail) {
+        const u32 d = dq[0];
+        for (u32 bi = 0; bi < tail; ++bi) hb_quad_cfb8_step<NR>(Q, rkq, P.rk, s, d >> (16 - 8 * bi));
+        const u32 sh = 32 - 8 * tail;
+        u32 word = hb_quad_s3_be(s) & (0xffffffffu >> sh);
+        if (nw == 0) word &= (P.topmask << (24 - sh)) | (0xffffffu >> sh);
+        HB_UNROLL
+        for (int t = NL - 1; t > 0; --t) out[t] = hb_alignbit(out[t], out[t - 1], sh);
+        out[0] = hb_alignbit(out[0], word << sh, sh);
+    }
+    u32 borrow = 0;
+    HB_UNROLL
+    for (int t = 0; t < NL; ++t) {
+        u64 d = (u64)out[t] - (u64)P.R[t] - (u64)borrow;
+        borrow = (u32)(d >> 63);
+    }
+    return borrow;
+}
+
+// hb_engine (MODE 0, fresh evaluations: h.init zeroes the register) with one
+// job per quad.  Only lane q = 0 of a quad takes jobs and calls h.accept; the
+// job index is broadcast to the quad.  `chunk` = jobs per refill per wave
+// (16 = one per quad).
+template <int NL, int NR, class H>
+__device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const PrfParams<NL> &P, u64 njobs,
+                                               unsigned long long *queue, u64 chunk) {
+    const QuadLane Q = hb_quad_lane(L);
+    const u32 q = hb_lane_id() & 3u;
+    const bool lead = q == 0;
+    u32 rkq[NR + 1];
+    HB_UNROLL
+    for (int r = 0; r <= NR; ++r)
+        rkq[r] = q == 0 ? P.rk[4 * r] : q == 1 ? P.rk[4 * r + 1] : q == 2 ? P.rk[4 * r + 2] : P.rk[4 * r + 3];
+    HbPool pool{0, 0, njobs, queue, false, chunk};
+    u64 job = 0;
+    bool active = pool.take(__ballot(lead), lead, job);
+    job = hb_qbcast64(job);
+    active = hb_qdpp<HB_QP(0, 0, 0, 0)>(active ? 1u : 0u) != 0;
+    u32 dig[8], s = 0, out[NL];
+    if (active) hb_job_digest<0>(h, job, dig, 0);
+    u32 tries = 0, job_tries = 0, failed = 0;
+    while (__ballot(active)) {
+        const u32 ok = hb_quad_prf_try<NL, NR>(Q, rkq, P, s, dig, out);
+        tries += active && lead ? 1u : 0u;
+        job_tries += 1u;
+        const bool acc = active && ok;
+        if (acc && lead) h.accept(job, out);
+        const bool give_up = active && !ok && job_tries >= HB_MAX_TRIES;
+        failed += give_up && lead ? 1u : 0u;
+        const bool next = acc || give_up;
+        const u64 m = __ballot(next && lead);
+        if (m) {
+            u64 nj = 0;
+            bool got = pool.take(m, next && lead, nj);
+            nj = hb_qbcast64(nj);
+            got = hb_qdpp<HB_QP(0, 0, 0, 0)>(got ? 1u : 0u) != 0;
+            if (next) {
+                active = got;
+                job = nj;
+                job_tries = 0;
+                if (got) {
+                    s = 0;   // fresh cipher per eval (util.py:88)
+                    hb_job_digest<0>(h, job, dig, 0);
+                }
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        tries += __shfl_xor(tries, off);
+        failed += __shfl_xor(failed, off);
+    }
+    if (hb_lane_id() == 0 && tries) atomicAdd(queue + 1, (unsigned long long)tries);
+    if (hb_lane_id() == 0 && failed) atomicAdd(queue + 2, (unsigned long long)failed);
+}
+
 // ------------------------------------------------------------------ encode
 // Minimum waves per SIMD requested from the register allocator: 4 (= one
 // 1024-thread workgroup, 16 waves per CU, sharing one 128 KiB LDS table
@@ -565,13 +735,16 @@ struct PrfHandler {
     }
 };
 
-template <int NL, int NR, int MODE>
+// QUAD: one evaluation per four lanes (hb_engine_quad, MODE 0 only) for
+// latency-bound batches.
+template <int NL, int NR, int MODE, bool QUAD = false>
 __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prf_kernel(PrfArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     PrfHandler<NL> h{A};
-    hb_engine<NL, NR, PrfHandler<NL>, MODE>(h, L, A.prf, A.n, A.queue, A.qchunk);
+    if constexpr (QUAD) hb_engine_quad<NL, NR, PrfHandler<NL>>(h, L, A.prf, A.n, A.queue, A.qchunk);
+    else hb_engine<NL, NR, PrfHandler<NL>, MODE>(h, L, A.prf, A.n, A.queue, A.qchunk);
 }
 
 // ------------------------------------------------------------------ Montgomery
@@ -619,7 +792,7 @@ struct ProveVHandler {
     }
 };
 
-template <int NL, int NR, int MODE_I, int MODE_V>
+template <int NL, int NR, int MODE_I, int MODE_V, bool QUAD = false>
 __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prove_prf_kernel(ProveArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
@@ -631,11 +804,13 @@ __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prove_prf_kernel(ProveArgs<NL
     const bool idx_half = !A.check_all && gridDim.x > 1 && blockIdx.x < gridDim.x / 2;
     if (!A.check_all && (idx_half || gridDim.x == 1)) {
         ProveIdxHandler<NL> hi{A};
-        hb_engine<2, NR, ProveIdxHandler<NL>, MODE_I>(hi, L, A.pi, A.n, A.queue, A.qchunk);
+        if constexpr (QUAD) hb_engine_quad<2, NR, ProveIdxHandler<NL>>(hi, L, A.pi, A.n, A.queue, A.qchunk);
+        else hb_engine<2, NR, ProveIdxHandler<NL>, MODE_I>(hi, L, A.pi, A.n, A.queue, A.qchunk);
     }
     if (!idx_half) {
         ProveVHandler<NL> hv{A};
-        hb_engine<NL, NR, ProveVHandler<NL>, MODE_V>(hv, L, A.pv, A.n, A.queue + HB_QSLOT, A.qchunk);
+        if constexpr (QUAD) hb_engine_quad<NL, NR, ProveVHandler<NL>>(hv, L, A.pv, A.n, A.queue + HB_QSLOT, A.qchunk);
+        else hb_engine<NL, NR, ProveVHandler<NL>, MODE_V>(hv, L, A.pv, A.n, A.queue + HB_QSLOT, A.qchunk);
     }
 }
 
@@ -817,23 +992,26 @@ hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass
 }
 
 
-// mode 0: KeyedPRF, 1: cxx prf (ByteCount(limit) % 16 == 0), 2: cxx prf (any limit)
+// mode 0: KeyedPRF, 1: cxx prf (ByteCount(limit) % 16 == 0), 2: cxx prf (any
+// limit), 3: KeyedPRF on the quad engine
 template <int NL>
 hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int mode, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
-#define HB_PRF_NR(M)                                                               \
-    do {                                                                           \
-        if (nr == 14) hipLaunchKernelGGL((hb_prf_kernel<NL, 14, M>), g, b, 0, s, A); \
-        else if (nr == 12) hipLaunchKernelGGL((hb_prf_kernel<NL, 12, M>), g, b, 0, s, A); \
-        else hipLaunchKernelGGL((hb_prf_kernel<NL, 10, M>), g, b, 0, s, A);       \
+#define HB_PRF_NR(M, Q)                                                               \
+    do {                                                                              \
+        if (nr == 14) hipLaunchKernelGGL((hb_prf_kernel<NL, 14, M, Q>), g, b, 0, s, A); \
+        else if (nr == 12) hipLaunchKernelGGL((hb_prf_kernel<NL, 12, M, Q>), g, b, 0, s, A); \
+        else hipLaunchKernelGGL((hb_prf_kernel<NL, 10, M, Q>), g, b, 0, s, A);       \
     } while (0)
     if (mode == 1) {
-        if constexpr (NL >= 4) HB_PRF_NR(1);   // cxx limits are >= 16 bytes
+        if constexpr (NL >= 4) HB_PRF_NR(1, false);   // cxx limits are >= 16 bytes
         else return hipErrorInvalidValue;
     } else if (mode == 2) {
-        HB_PRF_NR(2);
+        HB_PRF_NR(2, false);
+    } else if (mode == 3) {
+        HB_PRF_NR(0, true);
     } else {
-        HB_PRF_NR(0);
+        HB_PRF_NR(0, false);
     }
 #undef HB_PRF_NR
     return hipGetLastError();
@@ -855,19 +1033,21 @@ hipError_t hb_launch_wsum(const WsumArgs<NL> &A, int align, int gridx, hipStream
 }
 
 // stage 1 of prove; mode_i / mode_v: PRF modes of the index and v PRFs
-// (0 KeyedPRF; cxx prf: 1 whole blocks per try, 2 any limit)
+// (0 KeyedPRF; cxx prf: 1 whole blocks per try, 2 any limit; 3 KeyedPRF on the
+// quad engine, both)
 template <int NL>
 hipError_t hb_launch_prove_prf(const ProveArgs<NL> &A, int nr, int mode_i, int mode_v, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
-#define HB_PP(MI, MV)                                                                          \
-    do {                                                                                       \
-        if (nr == 14) hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 14, MI, MV>), g, b, 0, s, A); \
-        else if (nr == 12) hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 12, MI, MV>), g, b, 0, s, A); \
-        else hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 10, MI, MV>), g, b, 0, s, A);         \
+#define HB_PP(MI, MV, Q)                                                                          \
+    do {                                                                                          \
+        if (nr == 14) hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 14, MI, MV, Q>), g, b, 0, s, A); \
+        else if (nr == 12) hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 12, MI, MV, Q>), g, b, 0, s, A); \
+        else hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 10, MI, MV, Q>), g, b, 0, s, A);         \
     } while (0)
-    if (mode_i == 0 && mode_v == 0) HB_PP(0, 0);
-    else if (mode_v == 2) HB_PP(2, 2);
-    else if constexpr (NL >= 4) HB_PP(2, 1);
+    if (mode_i == 3 && mode_v == 3) HB_PP(0, 0, true);
+    else if (mode_i == 0 && mode_v == 0) HB_PP(0, 0, false);
+    else if (mode_v == 2) HB_PP(2, 2, false);
+    else if constexpr (NL >= 4) HB_PP(2, 1, false);
     else return hipErrorInvalidValue;
 #undef HB_PP
     return hipGetLastError();

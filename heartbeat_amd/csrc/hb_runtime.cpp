@@ -155,6 +155,20 @@ EngineShape small_engine(hb_ctx *c, u64 njobs) {
     return {(int)(g ? g : 1), 64};
 }
 
+// The quad engine (one KeyedPRF evaluation per four lanes, hb_engine_quad)
+// while four lanes per job still fit on the GPU at once: such launches are
+// bound by their longest serial CFB chain, not by throughput.  Every CU, one
+// job per quad per refill (16 per wave).
+bool use_quad(hb_ctx *c, u64 njobs) {
+    if (getenv("HB_NO_QUAD")) return false;   // A/B and parity tests: the lane engine
+    return njobs > 0 && 4 * njobs <= (u64)c->num_cus * HB_ENGINE_WG;
+}
+EngineShape quad_engine(hb_ctx *c, u64 njobs) {
+    u64 g = (njobs + 15) / 16;
+    if (g > (u64)c->num_cus) g = (u64)c->num_cus;
+    return {(int)(g ? g : 1), 16};
+}
+
 int check_key(hb_ctx *c, size_t key_len) {
     if (key_len != 16 && key_len != 24 && key_len != 32)
         return fail(c, HB_EINVAL, "AES key must be either 16, 24, or 32 bytes long");
@@ -179,10 +193,11 @@ int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_
     A.t0 = c->t0;
     A.queue = c->queue + HB_QSLOT * queue_slot;
     if (n == 0) return 0;
-    const EngineShape es = small_engine(c, n);
+    const bool quad = mode == 0 && use_quad(c, n);
+    const EngineShape es = quad ? quad_engine(c, n) : small_engine(c, n);
     A.qchunk = es.chunk;
     HB_CHECK(hipMemsetAsync(A.queue, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
-    HB_CHECK(hb_launch_prf<NL>(A, nr, mode, es.grid, c->stream), "hb_prf_kernel launch");
+    HB_CHECK(hb_launch_prf<NL>(A, nr, quad ? 3 : mode, es.grid, c->stream), "hb_prf_kernel launch");
     return 0;
 }
 
@@ -644,11 +659,13 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     c->last_launches = 0;
     HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
     c->prove_dirty = true;
-    const EngineShape es = small_engine(c, 2 * n);
+    const bool quad = !cxx && use_quad(c, 2 * n);
+    const EngineShape es = quad ? quad_engine(c, 2 * n) : small_engine(c, 2 * n);
     PA.qchunk = es.chunk;
     // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
     const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
-    HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, mode_i, mode_v, pgrid, c->stream), "hb_prove_prf_kernel launch");
+    HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, quad ? 3 : mode_i, quad ? 3 : mode_v, pgrid, c->stream),
+             "hb_prove_prf_kernel launch");
     c->last_launches++;
 
     // stage 2: mu_j = sum v_i m_{idx_i, j}, sigma = sum v_i tag[idx_i]   (PySwizzle.py:351-368)
