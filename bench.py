@@ -135,6 +135,8 @@ class Ranks(object):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # rehearsal of the N-rank path on a one-GPU box: every rank on device 0
+        self.device = 0 if os.environ.get("HB_BENCH_SAME_DEVICE") else self.local
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
@@ -229,7 +231,7 @@ def dry_run(args, R):
 def bench_encode(args, cfg, R):
     from heartbeat_amd import _native
     L = _native.lib()
-    ctx = _native.context(R.local)
+    ctx = _native.context(R.device)
     S = cfg["sectors"]
     p = P256
     pb = _native.be(p)
@@ -614,7 +616,7 @@ def bench_prove(args, cfg, R):
     mod-p reductions, with mu and sigma copied back to the host."""
     from heartbeat_amd import _native
     L = _native.lib()
-    ctx = _native.context(R.local)
+    ctx = _native.context(R.device)
     S = cfg["sectors"]
     p = P256
     pb = _native.be(p)

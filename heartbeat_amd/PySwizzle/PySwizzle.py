@@ -119,7 +119,7 @@ class Tag(object):
     @property
     def sigma(self):
         if self._sigma is None:
-            w, raw = self._width, self._raw
+            w, raw = self._width, bytes(self._raw)
             self._sigma = [int.from_bytes(raw[i:i + w], "big") for i in range(0, len(raw), w)]
         return self._sigma
 
@@ -367,10 +367,12 @@ def encode_file(p, sectors, f_key, alpha_key, file, devices=None):
     fb = FileBuffer(file)
     try:
         nblocks = fb.len // C + 1
+        # the tags land in the array the Tag keeps: no zero fill, no copy of
+        # the image (a bytes-like buffer to Tag)
         out = np.empty(nblocks * w, dtype=np.uint8)
         multi.encode_shards(p, sectors, fk, ak, fb.addr, fb.len, nblocks, out.ctypes.data, 0,
                             multi.devices(devices))
         fb.consume()
     finally:
         fb.close()
-    return Tag._from_raw(out.tobytes(), w), nblocks
+    return Tag._from_raw(out, w), nblocks

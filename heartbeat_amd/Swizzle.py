@@ -170,7 +170,7 @@ class Tag(_Serializable):
     @property
     def sigma(self):
         if self._sigma is None:
-            w, raw = self._width, self._raw
+            w, raw = self._width, bytes(self._raw)
             self._sigma = [int.from_bytes(raw[i:i + w], "big") for i in range(0, len(raw), w)]
         return self._sigma
 
@@ -192,7 +192,7 @@ class Tag(_Serializable):
         if self._sigma is None:
             w, raw = self._width, self._raw
             for i in range(0, len(raw), w):
-                v = raw[i:i + w].lstrip(b"\0") or b"\0"
+                v = bytes(raw[i:i + w]).lstrip(b"\0") or b"\0"
                 out.append(_u32(len(v)) + v)
         else:
             out.extend(_min_encoded(s) for s in self._sigma)
@@ -442,7 +442,7 @@ class Swizzle(_Serializable):
             fb.close()
         state.n = nblocks
         state.encrypt(self.k_enc, self.k_mac)
-        return Tag._from_raw(out.tobytes(), w), state
+        return Tag._from_raw(out, w), state
 
     def gen_challenge(self, state):
         """l = (unsigned int)(check_fraction * n) indices, v limit p (:704-729)."""

@@ -54,7 +54,14 @@ class FileBuffer(object):
                 try:
                     size = os.fstat(fd).st_size
                     if size > start:
-                        self._mm = mmap.mmap(fd, 0, access=mmap.ACCESS_READ)
+                        # encode reads every byte: prefault the mapping
+                        # (MAP_POPULATE) instead of taking page faults inside
+                        # the staging copies; prove reads only the challenged
+                        # blocks and maps lazily
+                        flags = mmap.MAP_SHARED
+                        if not from_start and hasattr(mmap, "MAP_POPULATE"):
+                            flags |= mmap.MAP_POPULATE
+                        self._mm = mmap.mmap(fd, 0, flags=flags, prot=mmap.PROT_READ)
                         arr = np.frombuffer(self._mm, dtype=np.uint8)[start:]
                     else:
                         arr = np.zeros(0, dtype=np.uint8)

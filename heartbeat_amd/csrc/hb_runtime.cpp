@@ -527,6 +527,8 @@ u32 wsum_grid(u64 nterms) {
     // one term per thread while the challenge is small (latency-bound
     // gathers), at most HB_WSUM_WG workgroups per column (the last one sums
     // the partials one per thread)
+    // (measured at 10,000 terms: 4 / 16 / 40 terms per thread take 1.2x /
+    // 2.7x / 7x as long -- the gathers of one thread do not overlap)
     u64 g = (nterms + HB_WSUM_WG - 1) / HB_WSUM_WG;
     if (g > HB_WSUM_WG) g = HB_WSUM_WG;
     return (u32)(g ? g : 1);
