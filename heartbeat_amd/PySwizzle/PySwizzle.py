@@ -375,4 +375,4 @@ def encode_file(p, sectors, f_key, alpha_key, file, devices=None):
         fb.consume()
     finally:
         fb.close()
-    return Tag._from_raw(out, w), nblocks
+    return Tag._from_raw(memoryview(out), w), nblocks

@@ -442,7 +442,7 @@ class Swizzle(_Serializable):
             fb.close()
         state.n = nblocks
         state.encrypt(self.k_enc, self.k_mac)
-        return Tag._from_raw(out, w), state
+        return Tag._from_raw(memoryview(out), w), state
 
     def gen_challenge(self, state):
         """l = (unsigned int)(check_fraction * n) indices, v limit p (:704-729)."""
