@@ -143,6 +143,13 @@ class Tag(object):
         top = 1 << (8 * w)
         return b"".join((s if 0 <= s < top else s % p).to_bytes(w, "big") for s in self.sigma)
 
+    def __getstate__(self):
+        # the encode image is a memoryview over the GPU output array: pickle bytes
+        d = dict(self.__dict__)
+        if d.get("_raw") is not None:
+            d["_raw"] = bytes(d["_raw"])
+        return d
+
     def todict(self):
         return {"sigma": self.sigma}
 

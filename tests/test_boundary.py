@@ -141,3 +141,22 @@ def test_no_gpu_fails_loudly():
     sw = Swizzle(1.0, 4, prime=(1 << 256) - 189)
     with pytest.raises(HeartbeatError):
         sw.encode(io.BytesIO(b"hello"))
+
+
+def test_pyswizzle_tag_image_pickles_and_compares():
+    """encode returns the tag image as a memoryview over its output array
+    (no copy); the Tag still pickles, deep-copies and converts like the
+    reference's list-of-ints Tag (PySwizzle.py:67-91)."""
+    import copy
+    import pickle
+
+    import numpy as np
+
+    from heartbeat_amd.PySwizzle.PySwizzle import Tag
+    arr = np.frombuffer(bytes(range(96)), dtype=np.uint8).copy()
+    t = Tag._from_raw(memoryview(arr), 32)
+    want = [int.from_bytes(bytes(range(k, k + 32)), "big") for k in (0, 32, 64)]
+    assert t.raw(2 ** 255 + 95) == bytes(range(96))
+    assert pickle.loads(pickle.dumps(t)).sigma == want
+    assert copy.deepcopy(t).sigma == want
+    assert len(t) == 3 and t.todict() == {"sigma": want}
