@@ -20,6 +20,7 @@ HB_TAGS_ON_DEVICE = 2
 HB_ENCODE_SINGLE_PASS = 4
 HB_EUNSUPPORTED = -4
 HB_PRF_CXX = 8
+HB_ASYNC = 16
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -65,6 +66,8 @@ SIGNATURES = [
     ("hb_host_unregister", _c.c_int, [_P, _P]),
     ("hb_fill_random", _c.c_int, [_P, _P, _c.c_uint64, _c.c_uint64]),
     ("hb_stream_read", _c.c_int, [_P, _P, _c.c_uint64, _c.POINTER(_c.c_double)]),
+    ("hb_ctx_set_stream", _c.c_int, [_P, _P]),
+    ("hb_ctx_wait", _c.c_int, [_P, _c.POINTER(_c.c_uint64)]),
     ("hb_merkle_offsets", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint64, _c.c_uint64, _c.c_uint64, _P]),
     ("hb_merkle_chunk_hmacs", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint64, _P, _c.c_uint64, _P,
                                          _c.c_uint64, _P]),

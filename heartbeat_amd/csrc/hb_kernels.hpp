@@ -130,6 +130,15 @@ __device__ __forceinline__ void hb_job_digest(const H &h, u64 job, u32 dig[8], l
     hb_prf_digest<MODE>(h.x_of(job), dig);
 }
 
+// Tries a job has already had before the engine sees it (the retry list: the
+// first pass ran one); the engine's give-up bound counts them.
+template <class H>
+__device__ __forceinline__ auto hb_resumed_tries(const H &, int) -> decltype(H::kResumedTries, u32()) {
+    return H::kResumedTries;
+}
+template <class H>
+__device__ __forceinline__ u32 hb_resumed_tries(const H &, long) { return 0u; }
+
 template <int NL, int NR, class H, int MODE = 0>
 __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParams<NL> &P,
                                           u64 njobs, unsigned long long *queue, u64 chunk = HB_QUEUE_CHUNK) {
@@ -141,7 +150,8 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
         h.init(job, sr);
         hb_job_digest<MODE>(h, job, dig, 0);
     }
-    u32 tries = 0, job_tries = 0, failed = 0;
+    const u32 resumed = hb_resumed_tries(h, 0);
+    u32 tries = 0, job_tries = resumed, failed = 0;
     while (__ballot(active)) {
         u32 ok;
         if constexpr (MODE == 1) ok = hb_cxx_try<NL, NR>(L, P, sr, dig, out);
@@ -165,7 +175,7 @@ __device__ __forceinline__ void hb_engine(H &h, const LaneTab &L, const PrfParam
             if (next) {
                 active = got;
                 job = nj;
-                job_tries = 0;
+                job_tries = resumed;
                 if (got) {
                     h.init(job, sr);   // fresh cipher per eval (util.py:88) or a resumed stream
                     hb_job_digest<MODE>(h, job, dig, 0);
@@ -469,7 +479,9 @@ __device__ __forceinline__ bool hb_block_full(const EncodeArgs<NL> &A, u64 job) 
 // The sector loads of a group go out HB_MFMA_BATCH at a time before their
 // MFMAs (one memory latency per batch, not per sector); the A fragments come
 // from LDS (`afl`, S <= HB_MFMA_LDS_S) or global memory.
+#ifndef HB_MFMA_BATCH
 #define HB_MFMA_BATCH 4
+#endif
 #define HB_MFMA_LDS_S 16
 template <int NL, bool ALDS>
 __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const hb_i32x4 *afl, u64 job, bool active,
@@ -676,6 +688,7 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
 
 template <int NL, int ALIGN>
 struct RetryHandler {
+    static constexpr u32 kResumedTries = 1;   // the first pass ran one try
     const EncodeArgs<NL> &A;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.block_base + A.retry[job].blk; }
     __device__ __forceinline__ void init(u64 job, u32 sr[4]) const {

@@ -78,6 +78,14 @@ struct hb_ctx {
     std::string err;
     double last_ms = 0.0;
     u32 last_launches = 0;
+    hipStream_t own_stream = nullptr;   // `stream` unless hb_ctx_set_stream gave another
+    // an HB_ASYNC encode still running: its counters, and the status and tries
+    // of the last one completed (hb_ctx_wait)
+    bool pending = false;
+    unsigned long long *pend_q0 = nullptr, *pend_q7 = nullptr;
+    int pend_rc = 0;
+    std::string pend_err;
+    u64 pend_tries = 0;
 };
 
 namespace {
@@ -325,6 +333,31 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17]) {
     return 0;
 }
 
+// Complete an HB_ASYNC encode: wait for its kernels, read its PRF counters;
+// the status is kept for hb_ctx_wait.  Every other entry point settles first
+// (its own kernels would reuse the counters and scratch buffers).
+void settle(hb_ctx *c) {
+    if (!c->pending) return;
+    c->pending = false;
+    const std::string keep = c->err;
+    auto done = [&](int rc) {
+        c->pend_rc = rc;
+        c->pend_err = rc ? c->err : std::string();
+        c->err = keep;
+    };
+    float ms = 0.f;
+    unsigned long long q[HB_QSLOT], r[HB_QSLOT];
+    hipError_t e = hipEventSynchronize(c->k1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->k0, c->k1);
+    if (e == hipSuccess) e = hipMemcpy(q, c->pend_q0, sizeof q, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(r, c->pend_q7, sizeof r, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return done(hipfail(c, e, "async encode"));
+    c->last_ms = ms;
+    if (q[2] || r[2]) return done(fail(c, HB_EINVAL, "PRF rejection sampling did not terminate for some blocks"));
+    c->pend_tries = q[1] + r[1];
+    done(check_prf_slots(c));
+}
+
 template <int NL>
 int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
                 const uint8_t *f_key, const uint8_t *a_key, size_t key_len, u64 block_base,
@@ -381,14 +414,20 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     u64 cb = C ? (256ull << 20) / C : 1;
     if (cb < 1) cb = 1;
     const u64 launch_blocks = data_dev ? nblocks : (nblocks < cb ? nblocks : cb);
+    // two passes (first tries with the prefix image, then the retry list) for
+    // PySwizzle; the cxx prf (2 AES per try, no prefix) runs single-pass: a
+    // cxx two-pass variant with the MFMA MAC measured 1,799 vs 2,246 GiB/s
+    // (profiles/r02/s8)
     const bool two_pass = !cxx && A.prf.nb >= 4 && !(flags & HB_ENCODE_SINGLE_PASS);
     if (two_pass) {
-        HB_CHECK(c->pfx.ensure(HB_PFX_BYTES), "hipMalloc(prefix)");
         A.retry_cap = retry_capacity(p_be, p_len, launch_blocks);
         HB_CHECK(c->retry.ensure((size_t)(A.retry_cap ? A.retry_cap : 1) * sizeof(HbRetry)), "hipMalloc(retry)");
-        A.pfx = (const unsigned char *)c->pfx.p;
         A.retry = (HbRetry *)c->retry.p;
         A.retry_count = q0 + 3;
+    }
+    if (two_pass && !cxx) {
+        HB_CHECK(c->pfx.ensure(HB_PFX_BYTES), "hipMalloc(prefix)");
+        A.pfx = (const unsigned char *)c->pfx.p;
         AesKey k;
         aes_expand(f_key, key_len, k);
         uint8_t zero[16] = {0}, o[16];
@@ -399,7 +438,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     float ms_total = 0.f;
     // the prefix image is part of the encode (rebuilt for every f_key): timed
     HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
-    if (two_pass) {
+    if (two_pass && !cxx) {
         PrefixArgs PA;
         memcpy(PA.rk, A.prf.rk, sizeof PA.rk);
         PA.t0 = c->t0;
@@ -427,7 +466,8 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         }
         HB_CHECK(hipMemsetAsync(q0 + 3, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
         A.queue = q0;
-        HB_CHECK(hb_launch_encode<NL>(A, nr, align, 1, engine_grid(c, nb), c->stream), "hb_encode_first_kernel launch");
+        HB_CHECK(hb_launch_encode<NL>(A, nr, align, 1, engine_grid(c, nb), c->stream),
+                 "hb_encode_first_kernel launch");
         HB_CHECK(hipMemsetAsync(q7, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
         A.queue = q7;
         HB_CHECK(hb_launch_encode<NL>(A, nr, align, 2, engine_grid(c, A.retry_cap), c->stream),
@@ -440,6 +480,13 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         rc = launch(data, len, nblocks, block_base, dtags);
         if (rc) return rc;
         HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
+        if (flags & HB_ASYNC) {
+            // kernels enqueued: hb_ctx_wait (or the next call) completes it
+            c->pending = true;
+            c->pend_q0 = q0;
+            c->pend_q7 = q7;
+            return 0;
+        }
         HB_CHECK(hipEventSynchronize(c->k1), "encode");
         HB_CHECK(hipEventElapsedTime(&ms_total, c->k0, c->k1), "hipEventElapsedTime");
     } else {
@@ -876,6 +923,7 @@ int hb_ctx_create(int device, hb_ctx **out) {
     }
     c->num_cus = prop.multiProcessorCount;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    c->own_stream = c->stream;
     if ((e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
     if ((e = hipEventCreate(&c->k0)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreate(&c->k1)) != hipSuccess) return bad(e, "hipEventCreate");
@@ -895,11 +943,12 @@ int hb_ctx_create(int device, hb_ctx **out) {
 void hb_ctx_destroy(hb_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    settle(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
                       &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
-                      &c->pfx, &c->retry, &c->ctl, &c->afrag};
+                      &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig};
     for (DevBuf *b : bufs) b->release();
     if (c->hres) (void)hipHostFree(c->hres);
     if (c->t0) (void)hipFree(c->t0);
@@ -910,9 +959,32 @@ void hb_ctx_destroy(hb_ctx *c) {
         if (c->copied[b]) (void)hipEventDestroy(c->copied[b]);
         if (c->done[b]) (void)hipEventDestroy(c->done[b]);
     }
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     delete c;
+}
+
+int hb_ctx_set_stream(hb_ctx *c, void *stream) {
+    if (!c) return HB_EINVAL;
+    settle(c);
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    // the previous stream's work (e.g. this context's own) is ordered before
+    // anything enqueued on the new one
+    HB_CHECK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    return 0;
+}
+
+int hb_ctx_wait(hb_ctx *c, uint64_t *tries_out) {
+    if (!c) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    settle(c);
+    const int rc = c->pend_rc;
+    if (rc) c->err = c->pend_err;
+    if (tries_out) *tries_out = c->pend_tries;
+    c->pend_rc = 0;
+    c->pend_tries = 0;
+    return rc;
 }
 
 const char *hb_last_error(const hb_ctx *c) { return c ? c->err.c_str() : g_create_error.c_str(); }
@@ -929,6 +1001,7 @@ static int prf_eval_common(hb_ctx *c, const uint8_t *key, size_t key_len, const 
                            size_t range_len, const uint64_t *xs, const uint8_t *digests, size_t n,
                            uint8_t *out) {
     if (!c) return HB_EINVAL;
+    settle(c);
     if (int rc = check_key(c, key_len)) return rc;
     const int bits = bitlen_be(range_be, range_len);
     if (bits == 0) return fail(c, HB_EINVAL, "PRF range must be positive");
@@ -991,6 +1064,7 @@ int hb_prf_eval_digests(hb_ctx *c, const uint8_t *key, size_t key_len, const uin
 int hb_cxx_prf_eval(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *limit_be,
                     size_t limit_len, const uint32_t *xs, size_t n, uint8_t *out) {
     if (!c) return HB_EINVAL;
+    settle(c);
     if (int rc = check_key(c, key_len)) return rc;
     const int bits = bitlen_be(limit_be, limit_len);
     if (bits == 0) return fail(c, HB_EINVAL, "PRF limit must be positive");
@@ -1031,6 +1105,7 @@ int hb_encode(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
               uint64_t block_base, const uint8_t *data, uint64_t len,
               uint64_t nblocks, uint8_t *tags, uint32_t flags, uint64_t *tries_out) {
     if (!c) return HB_EINVAL;
+    settle(c);
     PrimeInfo pi;
     if (int rc = parse_prime(c, p_be, p_len, pi)) return rc;
     if (int rc = check_key(c, key_len)) return rc;
@@ -1038,6 +1113,8 @@ int hb_encode(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sectors,
     if (!tags && nblocks) return fail(c, HB_EINVAL, "tags buffer is NULL");
     if (!data && len) return fail(c, HB_EINVAL, "data buffer is NULL");
     if (tries_out) *tries_out = 0;
+    if ((flags & HB_ASYNC) && (flags & (HB_DATA_ON_DEVICE | HB_TAGS_ON_DEVICE)) != (HB_DATA_ON_DEVICE | HB_TAGS_ON_DEVICE))
+        return fail(c, HB_EINVAL, "HB_ASYNC needs device-resident data and tags");
     if (nblocks == 0) return 0;
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     switch (pi.nl) {
@@ -1058,6 +1135,7 @@ int hb_prove_range(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sector
                    const uint8_t *vmax_be, size_t vmax_len, const uint8_t *tags, uint64_t ntags,
                    const uint8_t *data, uint64_t len, uint32_t flags, uint8_t *mu_out, uint8_t *sigma_out) {
     if (!c) return HB_EINVAL;
+    settle(c);
     PrimeInfo pi;
     if (int rc = parse_prime(c, p_be, p_len, pi)) return rc;
     if (int rc = check_key(c, key_len)) return rc;
@@ -1116,6 +1194,7 @@ static int verify_rhs(hb_ctx *c, const uint8_t *p_be, size_t p_len, uint32_t sec
                       uint64_t state_chunks, const uint8_t *chal_key, size_t chal_key_len, uint64_t chunks,
                       const uint8_t *vmax_be, size_t vmax_len, const uint8_t *mu, uint8_t *rhs_out, bool cxx) {
     if (!c) return HB_EINVAL;
+    settle(c);
     PrimeInfo pi;
     if (int rc = parse_prime(c, p_be, p_len, pi)) return rc;
     if (int rc = check_key(c, key_len)) return rc;
@@ -1167,6 +1246,7 @@ int hb_last_kernel_ms(const hb_ctx *c, double *ms, uint32_t *launches) {
 int hb_merkle_offsets(hb_ctx *c, const uint8_t *seeds, size_t seed_len, uint64_t nseeds, uint64_t filesz,
                       uint64_t chunksz, uint64_t *offsets) {
     if (!c) return HB_EINVAL;
+    settle(c);
     if (int rc = check_key(c, seed_len)) return rc;
     if (nseeds == 0) return 0;
     if (!seeds || !offsets) return fail(c, HB_EINVAL, "NULL buffer");
@@ -1213,6 +1293,7 @@ int hb_merkle_chunk_hmacs(hb_ctx *c, const uint8_t *seeds, size_t seed_len, uint
                           const uint8_t *data_dev, uint64_t len, const uint64_t *offsets, uint64_t chunk_len,
                           uint8_t *digests) {
     if (!c) return HB_EINVAL;
+    settle(c);
     if (seed_len == 0 || seed_len > 64) return fail(c, HB_EINVAL, "HMAC keys of 1..64 bytes");
     if (nseeds == 0) return 0;
     if (!seeds || !offsets || !digests || (!data_dev && chunk_len)) return fail(c, HB_EINVAL, "NULL buffer");
@@ -1246,6 +1327,7 @@ int hb_merkle_chunk_hmacs(hb_ctx *c, const uint8_t *seeds, size_t seed_len, uint
 
 int hb_fill_random(hb_ctx *c, uint8_t *dev_ptr, uint64_t len, uint64_t seed) {
     if (!c) return HB_EINVAL;
+    settle(c);
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     HB_CHECK(hb_launch_fill(dev_ptr, len, seed, c->stream), "hb_fill_kernel launch");
     HB_CHECK(hipStreamSynchronize(c->stream), "hb_fill_kernel");
@@ -1254,6 +1336,7 @@ int hb_fill_random(hb_ctx *c, uint8_t *dev_ptr, uint64_t len, uint64_t seed) {
 
 int hb_stream_read(hb_ctx *c, const void *dev_ptr, uint64_t len, double *ms) {
     if (!c || !dev_ptr) return HB_EINVAL;
+    settle(c);
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     if ((uintptr_t)dev_ptr % 16) return fail(c, HB_EINVAL, "hb_stream_read needs a 16-byte aligned buffer");
     HB_CHECK(c->sums.ensure(64), "hipMalloc");
@@ -1276,6 +1359,7 @@ int hb_device_malloc(hb_ctx *c, uint64_t bytes, void **out) {
 
 int hb_device_free(hb_ctx *c, void *p) {
     if (!c) return HB_EINVAL;
+    settle(c);
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     HB_CHECK(hipFree(p), "hipFree");
     return 0;
@@ -1297,6 +1381,7 @@ int hb_host_unregister(hb_ctx *c, void *ptr) {
 
 int hb_memcpy(hb_ctx *c, void *dst, const void *src, uint64_t bytes, int kind) {
     if (!c) return HB_EINVAL;
+    settle(c);
     HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
     hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     HB_CHECK(hipMemcpy(dst, src, bytes, k), "hipMemcpy");

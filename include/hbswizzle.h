@@ -50,6 +50,14 @@ extern "C" {
                           primes, 256-bit primes).  Tags differ from PySwizzle's.
                           Parity unpinned (Crypto++ absent). */
 
+#define HB_ASYNC 16u  /* hb_encode with device-resident data and tags: return once the
+                        encode kernels are enqueued on the context's stream (the
+                        prologue -- alpha PRF, MFMA fragments -- still completes
+                        first); hb_ctx_wait, or the context's next call, completes
+                        it.  With hb_ctx_set_stream the kernels run on the
+                        caller's stream ("an async variant takes a
+                        hipStream_t"). */
+
 /* error codes */
 #define HB_OK 0
 #define HB_EINVAL -1
@@ -73,6 +81,17 @@ void hb_ctx_destroy(hb_ctx *ctx);
 /* Message of the last error on this context (or of the last failed
  * hb_ctx_create when ctx is NULL). */
 const char *hb_last_error(const hb_ctx *ctx);
+
+/* Enqueue this context's kernels on `stream` (a hipStream_t of the
+ * context's device, e.g. torch.cuda.current_stream().cuda_stream), or on the
+ * context's own stream again with NULL.  Waits for the work already enqueued
+ * on the previous stream. */
+int hb_ctx_set_stream(hb_ctx *ctx, void *stream);
+
+/* Complete an HB_ASYNC hb_encode: wait for its kernels, check its PRF
+ * counters; its status is returned here (0 when none is pending) and *tries_out
+ * (may be NULL) receives its PRF tries.  Read the tags after this call. */
+int hb_ctx_wait(hb_ctx *ctx, uint64_t *tries_out);
 
 /* ceil(bitlen(p)/8): width of every tag / mu / sigma value. */
 size_t hb_width(const uint8_t *p_be, size_t p_len);

@@ -1,0 +1,70 @@
+"""GPU tests of the asynchronous C-ABI variant ("calls are
+synchronous; an async variant takes a hipStream_t"): hb_encode with HB_ASYNC
+returns once the encode kernels are enqueued, hb_ctx_wait completes it, and
+hb_ctx_set_stream puts the context's kernels on a caller's HIP stream.  Tags must equal the synchronous encode's."""
+import ctypes
+import hashlib
+
+import pytest
+
+from test_gpu_parity import P256, DevBuf
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def nat():
+    from heartbeat_amd import _native
+    _native.context()
+    return _native
+
+
+def test_async_encode_equals_sync(nat):
+    p, S, L = P256, 16, 16 << 20
+    nb = L // 512 + 1
+    pb = nat.be(p)
+    fk, ak = hashlib.sha256(b"async-f").digest(), hashlib.sha256(b"async-a").digest()
+    buf = DevBuf(nat, L)
+    tbs = [DevBuf(nat, nb * 32) for _ in range(4)]
+    ctx = nat.context()
+    L_ = nat.lib()
+    try:
+        ctx.check(L_.hb_fill_random(ctx.h, buf.p, L, 99))
+        tries = ctypes.c_uint64(0)
+        ctx.check(L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, buf.p, L, nb, tbs[0].p, 3, ctypes.byref(tries)))
+        # async + explicit wait
+        t2 = ctypes.c_uint64(123)
+        ctx.check(L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, buf.p, L, nb, tbs[1].p, 3 | nat.HB_ASYNC,
+                               ctypes.byref(t2)))
+        assert t2.value == 0                      # filled by hb_ctx_wait, not here
+        ctx.check(L_.hb_ctx_wait(ctx.h, ctypes.byref(t2)))
+        assert t2.value == tries.value
+        # async, then another call on the context settles it implicitly
+        ctx.check(L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, buf.p, L, nb, tbs[2].p, 3 | nat.HB_ASYNC, None))
+        got2 = tbs[2].download()
+        # on a caller's stream, created with the HIP runtime the library links
+        # (this image's torch bundles its own HIP runtime, a separate instance)
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        st = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+        ctx.check(L_.hb_ctx_set_stream(ctx.h, st))
+        try:
+            ctx.check(L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, buf.p, L, nb, tbs[3].p, 3 | nat.HB_ASYNC,
+                                   None))
+            assert hip.hipStreamSynchronize(st) == 0
+            ctx.check(L_.hb_ctx_wait(ctx.h, None))
+        finally:
+            ctx.check(L_.hb_ctx_set_stream(ctx.h, None))
+            hip.hipStreamDestroy(st)
+        want = tbs[0].download()
+        assert tbs[1].download() == want and got2 == want and tbs[3].download() == want
+        # nothing pending: wait is a no-op
+        ctx.check(L_.hb_ctx_wait(ctx.h, None))
+        # HB_ASYNC needs device data and tags
+        host = ctypes.create_string_buffer(L)
+        rc = L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, host, L, nb, tbs[0].p, 2 | nat.HB_ASYNC, None)
+        assert rc == -1 and b"HB_ASYNC" in L_.hb_last_error(ctx.h)
+    finally:
+        buf.free()
+        for tb in tbs:
+            tb.free()

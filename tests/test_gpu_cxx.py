@@ -197,3 +197,49 @@ def test_cxx_encode_64mib_vs_oracle(nat, oracle):
     finally:
         buf.free()
         tb.free()
+
+
+@pytest.mark.parametrize("p,S,L", [(P256, 16, 32 << 20), (P256, 4, 8 << 20), (P256, 10, 5 * 320 * 1000 + 77)])
+def test_cxx_encode_paths_agree(nat, oracle, monkeypatch, p, S, L):
+    """The cxx encode gives the same tags whatever the flags and environment
+    of the PySwizzle path (HB_ENCODE_SINGLE_PASS, a small HB_TEST_RETRY_CAP),
+    == the oracle from an aligned and a misaligned (+3 B) device pointer, and
+    through the chunked host path (ragged last chunk for L % C != 0).  (A cxx
+    two-pass variant with the MFMA MAC was measured slower and dropped,
+    DESIGN.md 5.2.)"""
+    ss = p.bit_length() // 8
+    C = ss * S
+    nb = L // C + 1
+    fk, ak = hashlib.sha256(b"cxx2-f").digest(), hashlib.sha256(b"cxx2-a").digest()
+    buf = DevBuf(nat, L + 16)
+    tbs = [DevBuf(nat, nb * 32) for _ in range(4)]
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L + 16, 4242))
+        pb = _be(p)
+        base = 3 | nat.HB_PRF_CXX
+
+        def enc(dptr, tptr, flags):
+            ctx.check(nat.lib().hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, dptr, L, nb, tptr, flags, None))
+
+        enc(buf.p, tbs[0].p, base)
+        enc(buf.p, tbs[1].p, base | nat.HB_ENCODE_SINGLE_PASS)
+        monkeypatch.setenv("HB_TEST_RETRY_CAP", "500")
+        enc(buf.p, tbs[2].p, base)
+        monkeypatch.delenv("HB_TEST_RETRY_CAP")
+        enc(buf.p + 3, tbs[3].p, base)
+        t = [tb.download() for tb in tbs]
+        assert t[0] == t[1] == t[2]
+        data = buf.download()
+        assert split_tags(t[0], 32) == oracle.cxx_encode(p, S, fk, ak, data[:L], nthreads=16)
+        assert split_tags(t[3], 32) == oracle.cxx_encode(p, S, fk, ak, data[3:3 + L], nthreads=16)
+        # host bytes (chunked H2D) == device-resident
+        host = ctypes.create_string_buffer(data[:L], L)
+        tags = ctypes.create_string_buffer(nb * 32)
+        ctx.check(nat.lib().hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, host, L, nb, tags, nat.HB_PRF_CXX,
+                                      None))
+        assert tags.raw == t[0]
+    finally:
+        buf.free()
+        for tb in tbs:
+            tb.free()
