@@ -316,10 +316,16 @@ __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const Prf
     const QuadLane Q = hb_quad_lane(L);
     const u32 q = hb_lane_id() & 3u;
     const bool lead = q == 0;
+    // rkq[r] = rk[4r + q]: select VALUES (readfirstlane: uniform SGPRs), not
+    // addresses -- a lane-dependent index into the kernel argument struct
+    // makes the compiler copy the whole struct to scratch
     u32 rkq[NR + 1];
     HB_UNROLL
-    for (int r = 0; r <= NR; ++r)
-        rkq[r] = q == 0 ? P.rk[4 * r] : q == 1 ? P.rk[4 * r + 1] : q == 2 ? P.rk[4 * r + 2] : P.rk[4 * r + 3];
+    for (int r = 0; r <= NR; ++r) {
+        const u32 k0 = __builtin_amdgcn_readfirstlane(P.rk[4 * r]), k1 = __builtin_amdgcn_readfirstlane(P.rk[4 * r + 1]);
+        const u32 k2 = __builtin_amdgcn_readfirstlane(P.rk[4 * r + 2]), k3 = __builtin_amdgcn_readfirstlane(P.rk[4 * r + 3]);
+        rkq[r] = q == 0 ? k0 : q == 1 ? k1 : q == 2 ? k2 : k3;
+    }
     HbPool pool{0, 0, njobs, queue, false, chunk};
     u64 job = 0;
     bool active = pool.take(__ballot(lead), lead, job);
@@ -393,7 +399,7 @@ struct EncodeHandler {
         }
         u32 tag[NL];
         hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
-        hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, tag);
+        hb_store_tag<NL, ALIGN>(A.tags + job * (u64)A.tw, A.tw, tag);
 #endif
     }
 };
@@ -615,7 +621,7 @@ __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const L
                 for (int t = 0; t < NL; ++t) F[t] = done ? out[t] : 0u;
                 hb_finish_T<NL>(T, F, A.mod, res);
                 if (done) {
-                    hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, res);
+                    hb_store_tag<NL, ALIGN>(A.tags + job * (u64)A.tw, A.tw, res);
                 } else {
                     *reinterpret_cast<uint4 *>(e->part) = make_uint4(res[0], res[1], res[2], res[3]);
                     *reinterpret_cast<uint4 *>(e->part + 4) = make_uint4(res[4], res[5], res[6], res[7]);
@@ -712,7 +718,7 @@ struct RetryHandler {
         } else {
             hb_block_tag<NL, ALIGN>(A.data, A.len, blk, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
         }
-        hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, tag);
+        hb_store_tag<NL, ALIGN>(A.tags + blk * (u64)A.tw, A.tw, tag);
     }
 };
 

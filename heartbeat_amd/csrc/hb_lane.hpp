@@ -792,6 +792,24 @@ HB_HD void hb_store_be(unsigned char *dst, u32 tw, const u32 v[NL]) {
     }
 }
 
+// hb_store_be for the kernels' sector-alignment class: ALIGN = 16 implies
+// ss == 4 NL, i.e. a prime of exactly 32 NL bits and tw == 4 NL -- NL
+// unconditional dword stores, none of the generic width's byte stores (whose
+// offsets would otherwise stay live in registers).
+template <int NL, int ALIGN>
+HB_HD void hb_store_tag(unsigned char *dst, u32 tw, const u32 v[NL]) {
+#if defined(HB_EXP_GENERIC_TAG_STORE)   // A/B: the generic store everywhere
+    if (0) {
+#else
+    if (ALIGN == 16) {
+#endif
+        HB_UNROLL
+        for (int t = 0; t < NL; ++t) *(u32 *)(dst + 4u * (u32)(NL - 1 - t)) = hb_bswap(v[t]);
+    } else {
+        hb_store_be<NL>(dst, tw, v);
+    }
+}
+
 // ------------------------------------------------------------------ block tag
 // Sector loads of a whole block.  ALIGN = 16: full-width sectors (ss == 4 NL,
 // e.g. a 256-bit prime with 32-byte sectors), ss, C and the data base all

@@ -711,6 +711,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     const bool quad = !cxx && use_quad(c, 2 * n);
     const EngineShape es = quad ? quad_engine(c, 2 * n) : small_engine(c, 2 * n);
     PA.qchunk = es.chunk;
+    const bool data_dev = flags & HB_DATA_ON_DEVICE, tags_dev = flags & HB_TAGS_ON_DEVICE;
     // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
     const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
     HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, quad ? 3 : mode_i, quad ? 3 : mode_v, pgrid, c->stream),
@@ -730,7 +731,6 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     A.ntags = ntags;
     A.qslots = PA.queue;
     A.nslots = 2;
-    const bool data_dev = flags & HB_DATA_ON_DEVICE, tags_dev = flags & HB_TAGS_ON_DEVICE;
     int rc = 0;
     if (data_dev && tags_dev) {
         A.mode = 0;

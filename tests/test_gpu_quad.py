@@ -75,3 +75,58 @@ def test_quad_prove_equals_lane_prove(oracle):
     finally:
         buf.free()
         tb.free()
+
+
+@pytest.mark.parametrize("prime_name,S,L,chunks", [("p256", 16, 8 << 20, 10000), ("p255", 5, 3 << 20, 3000),
+                                                   ("p1024", 10, 4 << 20, 700), ("p61", 4, 1 << 20, 20000),
+                                                   ("p256", 16, 1 << 20, 1)])
+def test_quad_prove_ranges_vs_oracle(oracle, prime_name, S, L, chunks):
+    """Device-resident proves on the quad engine == the lane engine
+    (HB_NO_QUAD=1) == the oracle, for several primes / sector counts (aligned
+    and byte-path sectors, 61- to 1024-bit), repeated on one context, and over
+    index ranges (hb_prove_range, i0 != 0) whose partial sums add up mod p."""
+    import json
+    from heartbeat_amd import _native as nat
+    from test_gpu_parity import DevBuf, dev_encode, split_tags
+    primes = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))
+    p = int(primes[prime_name], 16)
+    w = (p.bit_length() + 7) // 8
+    C = (p.bit_length() // 8) * S
+    nb = L // C + 1
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * w)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 31 + S))
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, tb.p)
+        key = hashlib.sha256(b"fused-%d" % chunks).digest()
+        pb = nat.be(p)
+
+        def prove(i0, i1, lane=False):
+            mu = ctypes.create_string_buffer(w * S)
+            sg = ctypes.create_string_buffer(w)
+            if lane:
+                os.environ["HB_NO_QUAD"] = "1"
+            try:
+                ctx.check(nat.lib().hb_prove_range(ctx.h, pb, len(pb), S, key, 32, chunks, i0, i1, pb, len(pb),
+                                                   tb.p, nb, buf.p, L, 3, mu, sg))
+            finally:
+                os.environ.pop("HB_NO_QUAD", None)
+            return mu.raw, sg.raw
+
+        full = prove(0, chunks)
+        assert full == prove(0, chunks, lane=True)
+        assert full == prove(0, chunks)
+        omu, osg = oracle.prove(p, S, key, chunks, p, split_tags(tb.download(), w), buf.download())
+        assert [int.from_bytes(full[0][j * w:(j + 1) * w], "big") for j in range(S)] == omu
+        assert int.from_bytes(full[1], "big") == osg
+        if chunks > 2:
+            cut = chunks // 3
+            a, b = prove(0, cut), prove(cut, chunks)
+            assert a == prove(0, cut, lane=True) and b == prove(cut, chunks, lane=True)
+            mu = [(int.from_bytes(a[0][j * w:(j + 1) * w], "big") + int.from_bytes(b[0][j * w:(j + 1) * w], "big")) % p
+                  for j in range(S)]
+            assert mu == omu
+    finally:
+        buf.free()
+        tb.free()
