@@ -711,7 +711,18 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     const bool quad = !cxx && use_quad(c, 2 * n);
     const EngineShape es = quad ? quad_engine(c, 2 * n) : small_engine(c, 2 * n);
     PA.qchunk = es.chunk;
-    const bool data_dev = flags & HB_DATA_ON_DEVICE, tags_dev = flags & HB_TAGS_ON_DEVICE;
+    const bool data_dev = flags & HB_DATA_ON_DEVICE;
+    bool tags_dev = flags & HB_TAGS_ON_DEVICE;
+    if (data_dev && !tags_dev) {
+        // device-resident file, host tags: upload the tags (1/S of the file's
+        // size at most) and gather on the device, instead of copying the
+        // whole file back to the host
+        HB_CHECK(c->tags.ensure((size_t)(ntags * pi.tw)), "hipMalloc(tags)");
+        HB_CHECK(hipMemcpyAsync(c->tags.p, tags, (size_t)(ntags * pi.tw), hipMemcpyHostToDevice, c->stream),
+                 "hipMemcpy(tags)");
+        tags = (const uint8_t *)c->tags.p;
+        tags_dev = true;
+    }
     // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
     const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
     HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, quad ? 3 : mode_i, quad ? 3 : mode_v, pgrid, c->stream),
@@ -763,15 +774,10 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
             HB_CHECK(hipMemcpy(tagbuf.data(), tags, tagbuf.size(), hipMemcpyDeviceToHost), "hipMemcpy(tags)");
         }
         const uint8_t *htags = tags_dev ? tagbuf.data() : tags;
-        std::vector<uint8_t> dbuf;
-        if (data_dev) {   // rare: device data with host tags
-            dbuf.resize((size_t)len);
-            HB_CHECK(hipMemcpy(dbuf.data(), data, (size_t)len, hipMemcpyDeviceToHost), "hipMemcpy(data)");
-        }
         // out-of-range indices (cxx prf after 81 tries) read as zero, reported at the end
         for (u64 i = 0; i < n; ++i)
             if (hidx[(size_t)i] >= ntags) hidx[(size_t)i] = 0;
-        Gather G{data_dev ? dbuf.data() : data, len, C, pi.ss, S, pi.tw, cxx, htags};
+        Gather G{data, len, C, pi.ss, S, pi.tw, cxx, htags};
         const u64 per = (u64)((256ull << 20) / (C + pi.tw)) ? (256ull << 20) / (C + pi.tw) : 1;
         const u64 bn = n < per ? n : per;
         HB_CHECK(c->data[0].ensure((size_t)(bn * C)), "hipMalloc(staging)");

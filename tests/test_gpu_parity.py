@@ -491,3 +491,36 @@ def test_device_resident_4_5gib_sampled_vs_oracle(nat, oracle):
     finally:
         buf.free()
         tb.free()
+
+
+def test_prove_mixed_residency_equals_device(nat, oracle):
+    """hb_prove with the file on the device and the tags on the host (the tags
+    are uploaded, the file is not copied back), and the other way round, ==
+    the all-device prove == the oracle."""
+    p, S, L = P256, 16, 16 << 20
+    nb = L // 512 + 1
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * 32)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 123))
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, tb.p)
+        htags = tb.download()
+        hdata = buf.download()
+        hd = ctypes.create_string_buffer(hdata, L)
+        ht = ctypes.create_string_buffer(htags, len(htags))
+        key = hashlib.sha256(b"mixed").digest()
+        pb = nat.be(p)
+        res = []
+        for tptr, dptr, flags in ((tb.p, buf.p, 3), (ht, buf.p, 1), (tb.p, hd, 2), (ht, hd, 0)):
+            mu = ctypes.create_string_buffer(32 * S)
+            sg = ctypes.create_string_buffer(32)
+            ctx.check(nat.lib().hb_prove(ctx.h, pb, 32, S, key, 32, 3000, pb, 32, tptr, nb, dptr, L, flags, mu, sg))
+            res.append((mu.raw, sg.raw))
+        assert res[0] == res[1] == res[2] == res[3]
+        omu, osg = oracle.prove(p, S, key, 3000, p, split_tags(htags, 32), hdata)
+        assert [int.from_bytes(res[0][0][j * 32:(j + 1) * 32], "big") for j in range(S)] == omu
+        assert int.from_bytes(res[0][1], "big") == osg
+    finally:
+        buf.free()
+        tb.free()
