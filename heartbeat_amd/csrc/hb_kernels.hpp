@@ -1072,9 +1072,14 @@ hipError_t hb_launch_prove_prf(const ProveArgs<NL> &A, int nr, int mode_i, int m
     return hipGetLastError();
 }
 
-#define HB_INST(NL)                                                                              \
-    template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t); \
+// Explicit instantiations per limb count; the encode and the PRF / prove
+// halves can go to separate translation units (parallel builds of the
+// slow-to-compile wide-limb kernels).
+#define HB_INST_ENC(NL) \
+    template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t);
+#define HB_INST_PRF(NL)                                                                          \
     template hipError_t hb_launch_prf<NL>(const PrfArgs<NL> &, int, int, int, hipStream_t);      \
     template hipError_t hb_launch_mont<NL>(const MontArgs<NL> &, hipStream_t);                   \
     template hipError_t hb_launch_wsum<NL>(const WsumArgs<NL> &, int, int, hipStream_t);         \
     template hipError_t hb_launch_prove_prf<NL>(const ProveArgs<NL> &, int, int, int, int, hipStream_t);
+#define HB_INST(NL) HB_INST_ENC(NL) HB_INST_PRF(NL)
