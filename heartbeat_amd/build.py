@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def build(jobs=5, verbose=False):
+def build(jobs=8, verbose=False):
     cmd = ["make", "-C", os.path.join(HERE, "csrc"), "-j%d" % jobs]
     if not verbose:
         cmd.insert(1, "-s")

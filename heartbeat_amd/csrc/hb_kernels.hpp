@@ -993,16 +993,16 @@ __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
 // limb count NL, AES rounds NR and sector alignment class).
 // pass: 0 = single-pass engine, 1 = first tries (prefix image), 2 = retry list,
 // 3 = cxx prf encode
-template <int NL>
-hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass, int grid, hipStream_t s) {
+template <int NL, int PASS>
+hipError_t hb_launch_encode_pass(const EncodeArgs<NL> &A, int nr, int align, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
 #define HB_ENC(K, NRV, AL) hipLaunchKernelGGL((K<NL, NRV, AL>), g, b, 0, s, A)
 #define HB_ENC_NR(K, AL) \
     do { if (nr == 14) HB_ENC(K, 14, AL); else if (nr == 12) HB_ENC(K, 12, AL); else HB_ENC(K, 10, AL); } while (0)
 #define HB_ENC_AL(K) do { if (align == 16) HB_ENC_NR(K, 16); else HB_ENC_NR(K, 1); } while (0)
-    if (pass == 1) HB_ENC_AL(hb_encode_first_kernel);
-    else if (pass == 2) HB_ENC_AL(hb_encode_retry_kernel);
-    else if (pass == 3) HB_ENC_AL(hb_cxx_encode_kernel);
+    if constexpr (PASS == 1) HB_ENC_AL(hb_encode_first_kernel);
+    else if constexpr (PASS == 2) HB_ENC_AL(hb_encode_retry_kernel);
+    else if constexpr (PASS == 3) HB_ENC_AL(hb_cxx_encode_kernel);
     else HB_ENC_AL(hb_encode_kernel);
 #undef HB_ENC_AL
 #undef HB_ENC_NR
@@ -1010,6 +1010,16 @@ hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass
     return hipGetLastError();
 }
 
+// One launcher per pass (hb_launch_encode_pass), so that the wide-limb
+// kernels of each pass can be instantiated in a translation unit of their own
+// (HB_INST_ENC_PASS) and built in parallel.
+template <int NL>
+hipError_t hb_launch_encode(const EncodeArgs<NL> &A, int nr, int align, int pass, int grid, hipStream_t s) {
+    if (pass == 1) return hb_launch_encode_pass<NL, 1>(A, nr, align, grid, s);
+    if (pass == 2) return hb_launch_encode_pass<NL, 2>(A, nr, align, grid, s);
+    if (pass == 3) return hb_launch_encode_pass<NL, 3>(A, nr, align, grid, s);
+    return hb_launch_encode_pass<NL, 0>(A, nr, align, grid, s);
+}
 
 // mode 0: KeyedPRF, 1: cxx prf (ByteCount(limit) % 16 == 0), 2: cxx prf (any
 // limit), 3: KeyedPRF on the quad engine
@@ -1077,6 +1087,14 @@ hipError_t hb_launch_prove_prf(const ProveArgs<NL> &A, int nr, int mode_i, int m
 // slow-to-compile wide-limb kernels).
 #define HB_INST_ENC(NL) \
     template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t);
+// the encode dispatcher alone, its passes instantiated elsewhere
+#define HB_EXTERN_ENC_PASSES(NL)                                                                  \
+    extern template hipError_t hb_launch_encode_pass<NL, 0>(const EncodeArgs<NL> &, int, int, int, hipStream_t); \
+    extern template hipError_t hb_launch_encode_pass<NL, 1>(const EncodeArgs<NL> &, int, int, int, hipStream_t); \
+    extern template hipError_t hb_launch_encode_pass<NL, 2>(const EncodeArgs<NL> &, int, int, int, hipStream_t); \
+    extern template hipError_t hb_launch_encode_pass<NL, 3>(const EncodeArgs<NL> &, int, int, int, hipStream_t);
+#define HB_INST_ENC_PASS(NL, P) \
+    template hipError_t hb_launch_encode_pass<NL, P>(const EncodeArgs<NL> &, int, int, int, hipStream_t);
 #define HB_INST_PRF(NL)                                                                          \
     template hipError_t hb_launch_prf<NL>(const PrfArgs<NL> &, int, int, int, hipStream_t);      \
     template hipError_t hb_launch_mont<NL>(const MontArgs<NL> &, hipStream_t);                   \
