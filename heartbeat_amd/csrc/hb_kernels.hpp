@@ -680,7 +680,12 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
         {
             u32 dig[8];
             hb_sha256_decimal(A.block_base + job, dig);
+            // waves in their AES phase go first in issue arbitration, so the
+            // LDS stays fed while other waves hash or run the MAC (+0.8 %,
+            // same-box A/B, profiles/r02/s13)
+            __builtin_amdgcn_s_setprio(2);
             ok = hb_prf_first_try<NL, NR>(L, A.prf, A.pfx, A.o0, sr, dig, out);
+            __builtin_amdgcn_s_setprio(0);
         }
         hb_first_finish<NL, NR, ALIGN>(A, L, h, job, act, ok, sr, out, tries, failed, T, tmine);
     }
