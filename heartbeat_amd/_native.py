@@ -21,6 +21,7 @@ HB_ENCODE_SINGLE_PASS = 4
 HB_EUNSUPPORTED = -4
 HB_PRF_CXX = 8
 HB_ASYNC = 16
+HB_BUILD_EXPERIMENT = 1
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -33,6 +34,7 @@ _P = _c.c_void_p
 _B = _c.c_char_p
 SIGNATURES = [
     ("hb_abi_version", _c.c_int, []),
+    ("hb_build_flags", _c.c_int, []),
     ("hb_device_count", _c.c_int, [_c.POINTER(_c.c_int)]),
     ("hb_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_P)]),
     ("hb_ctx_destroy", None, [_P]),
@@ -91,6 +93,10 @@ def lib():
                 f = getattr(L, name)
                 f.restype = res
                 f.argtypes = args
+            flags = L.hb_build_flags() if hasattr(L, "hb_build_flags") else 0
+            if flags & HB_BUILD_EXPERIMENT and not os.environ.get("HB_LIB_PATH"):
+                raise HeartbeatError("%s is an experiment build (HB_EXP_* switches may emit wrong "
+                                     "tags); rebuild the product library" % LIB_PATH)
             _lib = L
     return _lib
 

@@ -32,6 +32,17 @@
 typedef uint32_t u32;
 typedef uint64_t u64;
 
+// Instruction-count experiments (scripts/build_variant.sh) that make the
+// kernels emit WRONG tags.  They compile only together with
+// HB_EXPERIMENT_BUILD, which the product Makefile refuses for
+// libhbswizzle.so and which makes the library report itself as an experiment
+// build (hb_build_flags), so heartbeat_amd refuses it unless HB_LIB_PATH
+// selects it explicitly.
+#if (defined(HB_EXP_NO_SHA) || defined(HB_EXP_MAC_NOLOAD) || defined(HB_EXP_NO_MAC) || \
+     defined(HB_EXP_NO_FINISH) || defined(HB_EXP_NO_MFMA)) && !defined(HB_EXPERIMENT_BUILD)
+#error "HB_EXP_* switches produce wrong tags: experiment builds only (scripts/build_variant.sh)"
+#endif
+
 // ------------------------------------------------------------------ intrinsics
 HB_HD u32 hb_perm(u32 s0, u32 s1, u32 sel) {
 #if defined(__HIP_DEVICE_COMPILE__)

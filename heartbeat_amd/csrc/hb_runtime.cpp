@@ -890,6 +890,14 @@ extern "C" {
 
 int hb_abi_version(void) { return HB_ABI_VERSION; }
 
+int hb_build_flags(void) {
+#if defined(HB_EXPERIMENT_BUILD)
+    return HB_BUILD_EXPERIMENT;
+#else
+    return 0;
+#endif
+}
+
 int hb_device_count(int *n) {
     if (!n) return HB_EINVAL;
     *n = 0;

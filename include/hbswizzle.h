@@ -69,6 +69,12 @@ typedef struct hb_ctx hb_ctx;
 
 int hb_abi_version(void);
 
+/* Build properties.  HB_BUILD_EXPERIMENT: an A/B experiment build
+ * (scripts/build_variant.sh) whose HB_EXP_* switches may emit wrong tags; the
+ * Python package refuses such a library unless HB_LIB_PATH names it. */
+#define HB_BUILD_EXPERIMENT 1
+int hb_build_flags(void);
+
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens
  * one context per device; contexts fail on non-gfx950 devices). */
 int hb_device_count(int *n);

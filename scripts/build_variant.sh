@@ -6,5 +6,5 @@ set -e
 name=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 make -s -C "$ROOT/heartbeat_amd/csrc" -j${JOBS:-4} NL64=${NL64:-0} BUILD=build_$name OUT=../../exp_$name.so \
-  FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-pass-failed $*"
+  FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-pass-failed -DHB_EXPERIMENT_BUILD $*"
 echo "built exp_$name.so"

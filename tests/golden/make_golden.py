@@ -131,6 +131,23 @@ PRIMES = {
 }
 
 
+def next_prime(x):
+    """The smallest prime > x."""
+    x = x + 1 if x % 2 == 0 else x + 2
+    while not is_probable_prime(x):
+        x += 2
+    return x
+
+
+# Primes that only the repo's own tests use (no reference output is recorded
+# for them), kept in primes.json next to the reference-case primes:
+EXTRA_PRIMES = {
+    # the smallest 256-bit prime: the PRF's worst case, E[tries] = 2^256/p ~ 2
+    # (two-pass encode and retry-list-overflow tests, tests/test_gpu_parity.py)
+    "p256lo": next_prime(1 << 255),
+}
+
+
 def tags_digest(tags, width):
     h = hashlib.sha256()
     for t in tags:
@@ -269,7 +286,7 @@ def main():
                    "test6_sha256": hashlib.sha256(t6).hexdigest(),
                    "cases": big}, fh, indent=0)
     with open(os.path.join(out_dir, "primes.json"), "w") as fh:
-        json.dump({k: hex(v) for k, v in PRIMES.items()}, fh, indent=1)
+        json.dump({k: hex(v) for k, v in {**PRIMES, **EXTRA_PRIMES}.items()}, fh, indent=1)
 
 
 def position_cases(sw):

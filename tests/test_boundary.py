@@ -160,3 +160,25 @@ def test_pyswizzle_tag_image_pickles_and_compares():
     assert pickle.loads(pickle.dumps(t)).sigma == want
     assert copy.deepcopy(t).sigma == want
     assert len(t) == 3 and t.todict() == {"sigma": want}
+
+
+def test_product_build_is_not_an_experiment_build():
+    """The wrong-tag instruction-count switches (HB_EXP_*, hb_lane.hpp) cannot
+    reach libhbswizzle.so: the in-tree library reports a product build, the
+    headers refuse the switches without HB_EXPERIMENT_BUILD, and the product
+    Makefile refuses HB_EXP flags for libhbswizzle.so."""
+    import subprocess
+    from heartbeat_amd import _native
+    assert _native.lib().hb_build_flags() & _native.HB_BUILD_EXPERIMENT == 0
+    csrc = os.path.join(ROOT, "heartbeat_amd", "csrc")
+    src = '#include "hb_lane.hpp"\nint main() { return 0; }\n'
+    for flag in ("-DHB_EXP_NO_MAC", "-DHB_EXP_NO_SHA", "-DHB_EXP_MAC_NOLOAD"):
+        r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++", "-I", csrc, flag, "-"],
+                           input=src.encode(), capture_output=True)
+        assert r.returncode != 0 and b"experiment builds only" in r.stderr, flag
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++", "-I", csrc, "-DHB_EXP_NO_MAC",
+                        "-DHB_EXPERIMENT_BUILD", "-"], input=src.encode(), capture_output=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run(["make", "-n", "-C", csrc, "EXTRA=-DHB_EXP_NO_MAC -DHB_EXPERIMENT_BUILD"],
+                       capture_output=True)
+    assert r.returncode != 0 and b"not libhbswizzle.so" in r.stderr
