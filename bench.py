@@ -148,6 +148,25 @@ class Ranks(object):
         if self.dist is not None:
             self.dist.barrier()
 
+    def gather(self, obj):
+        """obj of every rank, in rank order (gloo all_gather_object)."""
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def device_report(self, bus_id):
+        """How many physically distinct GPUs the ranks ran on: an N-rank line
+        from a one-GPU rehearsal (HB_BENCH_SAME_DEVICE) must not read as N
+        GPUs."""
+        ids = self.gather((self.device, bus_id))
+        distinct = len({b if b is not None else "ordinal %d" % d for d, b in ids})
+        rep = {"distinct_devices": distinct, "device_pci_bus_ids": [b for _, b in ids]}
+        if os.environ.get("HB_BENCH_SAME_DEVICE"):
+            rep["same_device_rehearsal"] = True
+        return rep
+
     def reduce(self, x, op):
         """x (float) reduced over ranks with op in {"max", "min", "sum"}."""
         if self.dist is None:
@@ -218,9 +237,10 @@ def dry_run(args, R):
     R.barrier()
     elapsed = R.reduce(time.perf_counter() - t0, "max")
     blocks = R.reduce(plan["nblocks"], "sum")
+    rep = R.device_report(None)
     if R.rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": R.world,
-                          "steps": args.steps, "warmup": args.warmup,
+                          **rep, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
                           "scaling": "weak" if cfg["weak"] else "strong", "dry_run": True,
                           "config": {"workload": cfg["name"], "file_bytes": file_len,
@@ -345,6 +365,7 @@ def bench_encode(args, cfg, R):
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": R.world,
+        **R.device_report(_native.pci_bus_id(R.device)),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -655,7 +676,8 @@ def bench_prove(args, cfg, R):
     ms = R.reduce((time.perf_counter() - t0) / steps * 1e3, "max")
     line = {
         "metric": "Swizzle prove() latency, ms per proof (device-resident file and tags)",
-        "value": round(ms, 4), "unit": "ms", "n_gpus": R.world, "steps": steps, "warmup": args.warmup,
+        "value": round(ms, 4), "unit": "ms", "n_gpus": R.world,
+        **R.device_report(_native.pci_bus_id(R.device)), "steps": steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 4), "higher_is_better": False, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (SplitMix64 random file bytes, seeded keys)",

@@ -20,7 +20,7 @@ import hmac
 
 import numpy as np
 
-from .. import _native
+from .. import _native, multi
 from ..exc import HeartbeatError
 
 DEFAULT_CHUNK_SIZE = 8192     # Merkle.py:38
@@ -77,7 +77,7 @@ class MerkleHelper(object):
         if n == 0:
             return []
         out = np.zeros(n, dtype=np.uint64)
-        ctx = _native.context()
+        ctx = multi.primary_context()
         with ctx.lock:
             ctx.check(_native.lib().hb_merkle_offsets(ctx.h, blob, sl, n, int(filesz), int(chunksz),
                                                       out.ctypes.data))
@@ -133,7 +133,7 @@ class MerkleHelper(object):
             return [], []
         oarr = np.asarray(offs, dtype=np.uint64)
         dig = ctypes.create_string_buffer(32 * n)
-        ctx = _native.context()
+        ctx = multi.primary_context()
         with ctx.lock:
             ctx.check(_native.lib().hb_merkle_chunk_hmacs(ctx.h, blob, sl, n, data_ptr, int(length),
                                                           oarr.ctypes.data, int(chunksz), dig))

@@ -335,7 +335,7 @@ class PySwizzle(object):
         mub = b"".join((int(m) % p).to_bytes(w, "big") for m in mu[:S])
         vmax = _native.be(int(chal.v_max)) if chunks > 0 else b"\x01"
         rhs = ctypes.create_string_buffer(w)
-        ctx = _native.context()
+        ctx = multi.primary_context()
         pb = _native.be(p)
         fk, ak, ck = _kb(state.f_key), _kb(state.alpha_key), _kb(chal.key)
         with ctx.lock:

@@ -503,7 +503,7 @@ class Swizzle(_Serializable):
         mub = b"".join((int(m) % p).to_bytes(w, "big") for m in mu)
         vmax = _native.be(int(chal.v_max)) if chunks else b"\x01"
         rhs = ctypes.create_string_buffer(w)
-        ctx = _native.context()
+        ctx = multi.primary_context()
         pb = _native.be(p)
         fk, ak, ck = _kb(s.f_key), _kb(s.alpha_key), _kb(chal.key)
         with ctx.lock:

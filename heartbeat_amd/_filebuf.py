@@ -18,6 +18,19 @@ Two views, matching the two ways the reference touches the file:
 A read()-only object without ``seek`` cannot be rewound: it is read from its
 current position in both views (the reference's prove would fail on it with
 an AttributeError on ``seek``).
+
+Short reads.  The reference reads ``file.read(sectorsize)`` per sector and
+stops the encode at the FIRST read that returns fewer than ``sectorsize``
+bytes (PySwizzle.py:299-306; prove: :355-360), treating it as end of file.
+For seekable files, BytesIO and any blocking file object that returns short
+reads only at EOF, that is exactly "the bytes up to EOF", which is what the
+buffer here holds.  An object that returns short reads MID-stream (an
+unbuffered socket, a raw pipe, an io.RawIOBase reader) makes the reference
+truncate the tags at the first short read -- at a point that depends on the
+sizes its reads happened to return, not on the data -- while the fallback
+below reads such an object to EOF with one ``read()`` and tags all of it.
+Wrap such streams in ``io.BufferedReader`` (or read them into a BytesIO)
+first if the reference's truncation is wanted; INTEGRATION.md section 6.
 """
 import io
 import mmap
@@ -68,6 +81,9 @@ class FileBuffer(object):
                 except (OSError, ValueError):
                     arr = None
             if arr is None:
+                # a file-like object without a usable fd: one read() to EOF
+                # (see "Short reads" above for how this differs from the
+                # reference on streams that return short reads mid-stream)
                 if from_start:
                     try:
                         file.seek(0)

@@ -36,6 +36,7 @@ SIGNATURES = [
     ("hb_abi_version", _c.c_int, []),
     ("hb_build_flags", _c.c_int, []),
     ("hb_device_count", _c.c_int, [_c.POINTER(_c.c_int)]),
+    ("hb_device_pci_bus_id", _c.c_int, [_c.c_int, _P, _c.c_size_t]),
     ("hb_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_P)]),
     ("hb_ctx_destroy", None, [_P]),
     ("hb_last_error", _c.c_char_p, [_P]),
@@ -99,6 +100,14 @@ def lib():
                                      "tags); rebuild the product library" % LIB_PATH)
             _lib = L
     return _lib
+
+
+def pci_bus_id(device):
+    """PCI bus id of a device (None if it cannot be queried)."""
+    buf = ctypes.create_string_buffer(64)
+    if lib().hb_device_pci_bus_id(int(device), buf, 64) != 0:
+        return None
+    return buf.value.decode("ascii", "replace")
 
 
 def default_device():

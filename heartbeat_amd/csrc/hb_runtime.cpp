@@ -246,8 +246,8 @@ int parse_prime(hb_ctx *c, const uint8_t *p_be, size_t p_len, PrimeInfo &pi) {
     if (pi.bits < 8) return fail(c, HB_EINVAL, "prime must be at least 2^7 (sector size >= 1 byte)");
     if (!(p_be[p_len - 1] & 1)) return fail(c, HB_EINVAL, "prime must be odd");
     pi.nl = nl_for_bits(pi.bits);
-    if (pi.nl < 8) pi.nl = 8;
     if (!pi.nl) return fail(c, HB_EUNSUPPORTED, "primes above 2048 bits are not supported by this build");
+    if (pi.nl < 8) pi.nl = 8;
     pi.ss = (u32)pi.bits / 8;
     pi.tw = (u32)(pi.bits + 7) / 8;
     return 0;
@@ -340,9 +340,13 @@ void settle(hb_ctx *c) {
     if (!c->pending) return;
     c->pending = false;
     const std::string keep = c->err;
+    // the FIRST failure since the last hb_ctx_wait is kept: a second async
+    // encode issued before the wait must not hide the first one's error
     auto done = [&](int rc) {
-        c->pend_rc = rc;
-        c->pend_err = rc ? c->err : std::string();
+        if (rc && c->pend_rc == 0) {
+            c->pend_rc = rc;
+            c->pend_err = c->err;
+        }
         c->err = keep;
     };
     float ms = 0.f;
@@ -354,7 +358,7 @@ void settle(hb_ctx *c) {
     if (e != hipSuccess) return done(hipfail(c, e, "async encode"));
     c->last_ms = ms;
     if (q[2] || r[2]) return done(fail(c, HB_EINVAL, "PRF rejection sampling did not terminate for some blocks"));
-    c->pend_tries = q[1] + r[1];
+    c->pend_tries += q[1] + r[1];
     done(check_prf_slots(c));
 }
 
@@ -907,6 +911,13 @@ int hb_device_count(int *n) {
     return 0;
 }
 
+int hb_device_pci_bus_id(int device, char *out, size_t n) {
+    if (!out || n < 16) return HB_EINVAL;
+    out[0] = 0;
+    if (hipDeviceGetPCIBusId(out, (int)n, device) != hipSuccess) return HB_EHIP;
+    return 0;
+}
+
 int hb_ctx_create(int device, hb_ctx **out) {
     if (!out) return HB_EINVAL;
     *out = nullptr;
@@ -1251,6 +1262,12 @@ int hb_aes_cfb128(const uint8_t *key, size_t key_len, const uint8_t *iv, const u
 
 int hb_last_kernel_ms(const hb_ctx *c, double *ms, uint32_t *launches) {
     if (!c) return HB_EINVAL;
+    // a pending HB_ASYNC encode is the last one: complete it first (its status
+    // stays for hb_ctx_wait)
+    if (c->pending) {
+        hb_ctx *m = const_cast<hb_ctx *>(c);
+        if (hipSetDevice(m->device) == hipSuccess) settle(m);
+    }
     if (ms) *ms = c->last_ms;
     if (launches) *launches = c->last_launches;
     return 0;

@@ -15,16 +15,22 @@ One host thread per device; ctypes releases the GIL during the calls, so the
 devices run concurrently (and, for host-resident files, so do their PCIe
 links).
 
-Device selection: ``set_devices([...])``, or $HB_DEVICES ("0,1,2,3" or
-"all"); by default every visible device.  Small jobs stay on one device:
-a shard gets at least MIN_SHARD_BYTES of file (encode) or MIN_SHARD_CHUNKS
-challenge indices (prove).
+Device selection, first match wins: ``set_devices([...])``; $HB_DEVICES
+("0,1,2,3" or "all"); $HB_DEVICE (one device: the process is pinned); under a
+launcher ($LOCAL_RANK) the rank's device; otherwise every visible device.
+Every call of the drop-in API -- encode, prove, verify, KeyedPRF, Merkle --
+uses ``devices()[0]`` as its single device, so one flow never touches a GPU
+outside the selection.  Small jobs stay on one device: a shard gets at least
+MIN_SHARD_BYTES of file (encode) or MIN_SHARD_CHUNKS challenge indices
+(prove).  Device-resident buffers (HB_DATA_ON_DEVICE / HB_TAGS_ON_DEVICE) are
+one device's memory: they are refused with more than one distinct device.
 """
 import ctypes
 import os
 import threading
 
 from . import _native
+from .exc import HeartbeatError
 from .shard import block_range, shard_plan
 
 MIN_SHARD_BYTES = 256 << 20
@@ -54,11 +60,26 @@ def devices(explicit=None):
     env = os.environ.get("HB_DEVICES", "").strip()
     if env and env != "all":
         return [int(x) for x in env.split(",") if x.strip()]
-    if env == "all" or "LOCAL_RANK" not in os.environ:
+    pinned = any(os.environ.get(v, "").strip() for v in ("HB_DEVICE", "LOCAL_RANK"))
+    if env == "all" or not pinned:
         n = visible_device_count()
         if n > 0:
             return list(range(n))
     return [_native.default_device()]
+
+
+def primary_context():
+    """The context of the first selected device: single-device calls
+    (verify, KeyedPRF, Merkle) run where encode and prove run."""
+    return _native.context(devices()[0])
+
+
+def check_resident(flags, devs):
+    """Device-resident input or output is one device's memory: no peer access
+    is set up, so it cannot be split over several devices."""
+    if flags & (_native.HB_DATA_ON_DEVICE | _native.HB_TAGS_ON_DEVICE) and len(set(devs)) > 1:
+        raise HeartbeatError("device-resident buffers cannot be sharded over devices %s: "
+                             "pass one device, or host buffers" % sorted(set(devs)))
 
 
 def contexts(devs):
@@ -105,6 +126,7 @@ def encode_shards(p, sectors, fk, ak, addr, length, nblocks, out_addr, flags, de
     w = _native.width_of(p)
     C = (p.bit_length() // 8) * sectors
     G = shard_count(len(devs), length, min_bytes)
+    check_resident(flags, devs[:G])
     ctxs = contexts(devs[:G])
     pb = _native.be(p)
     L = _native.lib()
@@ -132,6 +154,7 @@ def prove_shards(p, sectors, key, chunks, vmax_be, tags_addr, ntags, data_addr, 
     (mu, sigma) added mod p.  Returns (mu list, sigma)."""
     w = _native.width_of(p)
     G = shard_count(len(devs), chunks, min_chunks)
+    check_resident(flags, devs[:G])
     ctxs = contexts(devs[:G])
     pb = _native.be(p)
     L = _native.lib()

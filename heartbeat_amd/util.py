@@ -6,7 +6,7 @@ import hashlib
 
 import numpy as np
 
-from . import _native
+from . import _native, multi
 from .exc import HeartbeatError
 
 
@@ -64,7 +64,7 @@ class KeyedPRF(object):
         key = _key_bytes(self.key)
         nb = (rng.bit_length() + 7) // 8
         out = ctypes.create_string_buffer(nb * len(xs))
-        ctx = _native.context()
+        ctx = multi.primary_context()
         rb = _native.be(rng)
         if all(0 <= x < 1 << 64 for x in xs):
             # the kernel hashes decimal(x) itself

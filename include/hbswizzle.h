@@ -79,6 +79,11 @@ int hb_build_flags(void);
  * one context per device; contexts fail on non-gfx950 devices). */
 int hb_device_count(int *n);
 
+/* PCI bus id ("dddd:bb:dd.f", NUL-terminated, n >= 16) of HIP device
+ * `device`: tells physically distinct GPUs apart (bench.py's
+ * distinct_devices) whatever ordinal remapping a launcher applies. */
+int hb_device_pci_bus_id(int device, char *out, size_t n);
+
 /* Open a context on HIP device `device`.  Replaces nothing in the reference
  * (it runs on the host only); the reference's per-call state lives in
  * PySwizzle objects (PySwizzle.py:233-255). */
@@ -95,8 +100,10 @@ const char *hb_last_error(const hb_ctx *ctx);
 int hb_ctx_set_stream(hb_ctx *ctx, void *stream);
 
 /* Complete an HB_ASYNC hb_encode: wait for its kernels, check its PRF
- * counters; its status is returned here (0 when none is pending) and *tries_out
- * (may be NULL) receives its PRF tries.  Read the tags after this call. */
+ * counters.  Returns the status of the async encodes completed since the last
+ * hb_ctx_wait -- the FIRST failure among them, 0 if none failed -- and
+ * *tries_out (may be NULL) receives their PRF tries.  Read the tags after
+ * this call. */
 int hb_ctx_wait(hb_ctx *ctx, uint64_t *tries_out);
 
 /* ceil(bitlen(p)/8): width of every tag / mu / sigma value. */
@@ -243,7 +250,9 @@ int hb_aes_cfb128(const uint8_t *key, size_t key_len, const uint8_t *iv,
                   const uint8_t *in, uint8_t *out, size_t n, int encrypt);
 
 /* Device timing of the last hb_encode on this context: milliseconds spent in
- * the encode kernel (HIP events on the kernel's stream), and launch count. */
+ * the encode kernel (HIP events on the kernel's stream), and launch count.  A
+ * pending HB_ASYNC encode is completed first (its status stays for
+ * hb_ctx_wait). */
 int hb_last_kernel_ms(const hb_ctx *ctx, double *ms, uint32_t *launches);
 
 /* Device memory helpers so that callers without a GPU framework (e.g. a cgo or

@@ -11,10 +11,11 @@ import sys
 from conftest import ROOT
 
 
-def _run(*args):
+def _run(*args, extra_env=None):
     env = dict(os.environ)
-    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "HB_BENCH_SAME_DEVICE"):
         env.pop(k, None)
+    env.update(extra_env or {})
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"] + list(args),
                          capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
@@ -30,11 +31,20 @@ def test_two_ranks_one_line():
     # rank 1 sleeps 4 ms per step, rank 0 2 ms: the max over ranks is reported
     assert d["ms_per_step"] >= 3.5
     assert d["config"]["blocks_summed"] == d["config"]["blocks_total"]
+    assert d["distinct_devices"] == 2 and "same_device_rehearsal" not in d
+
+
+def test_same_device_rehearsal_is_marked():
+    """Two ranks on one GPU (HB_BENCH_SAME_DEVICE) report n_gpus = 2 but
+    distinct_devices = 1 and same_device_rehearsal: such a line can never
+    pass for a 2-GPU measurement."""
+    d = _run("--gpus", "2", "--steps", "1", extra_env={"HB_BENCH_SAME_DEVICE": "1"})
+    assert d["n_gpus"] == 2 and d["distinct_devices"] == 1 and d["same_device_rehearsal"] is True
 
 
 def test_single_rank():
     d = _run("--steps", "2")
-    assert d["n_gpus"] == 1 and d["scaling"] == "weak"
+    assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["distinct_devices"] == 1
     assert d["config"]["file_bytes"] == 64 << 30
 
 

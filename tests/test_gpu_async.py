@@ -68,3 +68,42 @@ def test_async_encode_equals_sync(nat):
         buf.free()
         for tb in tbs:
             tb.free()
+
+
+def test_async_status_and_timing_accumulate(nat):
+    """Two HB_ASYNC encodes before one hb_ctx_wait: the wait reports both
+    (tries summed; a failure of the first would be kept), and
+    hb_last_kernel_ms completes a pending encode instead of reporting the
+    previous operation's time."""
+    p, S, L = P256, 16, 8 << 20
+    nb = L // 512 + 1
+    pb = nat.be(p)
+    fk, ak = hashlib.sha256(b"async2-f").digest(), hashlib.sha256(b"async2-a").digest()
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * 32)
+    ctx = nat.context()
+    L_ = nat.lib()
+    try:
+        ctx.check(L_.hb_fill_random(ctx.h, buf.p, L, 7))
+        tries = ctypes.c_uint64(0)
+        ctx.check(L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, buf.p, L, nb, tb.p, 3, ctypes.byref(tries)))
+        sync_ms, _ = ctx.last_kernel_ms()
+        want = tb.download()
+        for _ in range(2):
+            ctx.check(L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, buf.p, L, nb, tb.p, 3 | nat.HB_ASYNC, None))
+        t2 = ctypes.c_uint64(0)
+        ctx.check(L_.hb_ctx_wait(ctx.h, ctypes.byref(t2)))
+        assert t2.value == 2 * tries.value
+        # a tiny synchronous PRF batch sets the timing to its own; the async
+        # encode after it must be what hb_last_kernel_ms reports
+        ctx.check(L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, buf.p, 512, 2, tb.p, 3, None))
+        small_ms, _ = ctx.last_kernel_ms()
+        ctx.check(L_.hb_encode(ctx.h, pb, 32, S, fk, ak, 32, 0, buf.p, L, nb, tb.p, 3 | nat.HB_ASYNC, None))
+        big_ms, launches = ctx.last_kernel_ms()
+        assert big_ms > 2 * small_ms and 0.5 * sync_ms < big_ms < 2 * sync_ms and launches >= 1
+        ctx.check(L_.hb_ctx_wait(ctx.h, ctypes.byref(t2)))
+        assert t2.value == tries.value
+        assert tb.download() == want
+    finally:
+        buf.free()
+        tb.free()

@@ -133,3 +133,44 @@ def test_prove_partition_sums_mod_p(oracle):
     parts = [part(0, 13), part(13, 27), part(27, 40)]
     assert [sum(x[0][j] for x in parts) % p for j in range(S)] == mu
     assert sum(x[1] for x in parts) % p == sg
+
+
+def test_hb_device_pins_every_call(monkeypatch):
+    """$HB_DEVICE pins the process to one device: encode, prove and the
+    single-device calls (verify, KeyedPRF, Merkle: multi.primary_context)
+    all resolve to it, whatever the visible device count."""
+    from heartbeat_amd import multi
+    monkeypatch.delenv("HB_DEVICES", raising=False)
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    monkeypatch.setattr(multi, "visible_device_count", lambda: 8)
+    assert multi.devices() == list(range(8))          # unpinned: every device
+    monkeypatch.setenv("HB_DEVICE", "3")
+    assert multi.devices() == [3]
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert multi.devices() == [3]                     # HB_DEVICE before LOCAL_RANK
+    monkeypatch.delenv("HB_DEVICE")
+    assert multi.devices() == [5]
+    monkeypatch.setenv("HB_DEVICES", "6,7")
+    assert multi.devices() == [6, 7]                  # an explicit list wins
+    opened = []
+    monkeypatch.setattr(multi._native, "context", lambda d=None, k=0: opened.append(d) or d)
+    assert multi.primary_context() == 6 and opened == [6]
+
+
+def test_device_resident_buffers_refuse_several_devices():
+    """HB_DATA_ON_DEVICE / HB_TAGS_ON_DEVICE pointers belong to one device:
+    sharding them over distinct devices is refused before any call."""
+    from heartbeat_amd import multi, _native
+    from heartbeat_amd.exc import HeartbeatError
+    for flags in (_native.HB_DATA_ON_DEVICE, _native.HB_TAGS_ON_DEVICE,
+                  _native.HB_DATA_ON_DEVICE | _native.HB_TAGS_ON_DEVICE):
+        with pytest.raises(HeartbeatError, match="device-resident"):
+            multi.check_resident(flags, [0, 1])
+        with pytest.raises(HeartbeatError):
+            multi.encode_shards(P256, 16, b"f" * 32, b"a" * 32, 1 << 20, 4 << 30, (4 << 30) // 512 + 1,
+                                1 << 20, flags, [0, 1, 0, 1])
+        with pytest.raises(HeartbeatError):
+            multi.prove_shards(P256, 16, b"k" * 32, 1 << 22, P256.to_bytes(32, "big"), 1 << 20, 100,
+                               1 << 20, 4 << 30, flags, [2, 3])
+        multi.check_resident(flags, [1, 1])            # one device (two contexts): fine
+    multi.check_resident(0, [0, 1])                    # host buffers shard freely
