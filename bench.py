@@ -423,7 +423,7 @@ def bench_encode(args, cfg, R):
     if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
         if len(pieces) > 1:
             fill(0)
-        line["cpu_baseline"] = cpu_baseline(ctx, L, dptr, pieces[0][1], S, p, fk, ak, C,
+        line["cpu_baseline"] = cpu_baseline(ctx, L, dptr, tptr, pieces[0][1], S, p, fk, ak, C,
                                             args.cpu_seconds, args.cpu_threads, args.py_seconds, cxx)
     if R.rank == 0 and args.host_path:
         line["host_path"] = host_path(ctx, L, dptr, pieces[0][1], S, pb, fk, ak, C)
@@ -494,11 +494,17 @@ def host_cpu_info():
     return info
 
 
-def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads, py_seconds, cxx=False):
-    """Oracle (kind "port") on successive 256 MiB prefixes of the same file
-    until `seconds` of CPU work, on this process's CPU share; plus the
-    single-core pure-Python PySwizzle restatement on 1 MiB and a bounded
-    prefix of a 64 MiB input."""
+def cpu_baseline(ctx, L, dptr, tptr, length, S, p, fk, ak, C, seconds, threads, py_seconds, cxx=False):
+    """CPU rows on this process's CPU share, on prefixes of the SAME synthetic
+    file (copied from the device in 256 MiB pieces):
+      * headline ("cxx Swizzle" counterpart): the native
+        multi-threaded encoder baseline/hb_cpu_swizzle.cpp (AES-NI CFB-8,
+        SHA-NI, 64-bit-limb Montgomery MAC, std::thread) until `seconds` of
+        work; its tags are compared with the GPU's for the same blocks;
+      * the test oracle (OpenSSL EVP + BIGNUM per sector) for a third of that;
+      * the single-core pure-Python PySwizzle restatement on 1 MiB and a
+        bounded prefix of a 64 MiB input.
+    The cxx-PRF mode has no native row (the oracle is its headline)."""
     import io
     import numpy as np
     from oracle import oracle as O
@@ -511,30 +517,59 @@ def cpu_baseline(ctx, L, dptr, length, S, p, fk, ak, C, seconds, threads, py_sec
     piece = (256 << 20) // C * C
     host = np.empty(piece, dtype=np.uint8)
     out = np.empty((piece // C) * 32, dtype=np.uint8)
-    done = 0
-    busy = 0.0
-    off = 0
-    while busy < seconds and off < length:
-        n = min(piece, length - off)
-        ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value + off, n, 2))
-        nb = n // C
-        t = time.perf_counter()
-        rc = O.encode_raw(p, S, fk, ak, host.ctypes.data, n, off // C, nb, out.ctypes.data, threads, cxx)
-        busy += time.perf_counter() - t
+    gpu = np.empty((piece // C) * 32, dtype=np.uint8)
+
+    def timed(encode, budget):
+        done = busy = 0.0
+        off = 0
+        same = True
+        while busy < budget and off < length:
+            n = min(piece, length - off)
+            ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value + off, n, 2))
+            nb = n // C
+            t = time.perf_counter()
+            encode(off // C, n, nb)
+            busy += time.perf_counter() - t
+            ctx.check(L.hb_memcpy(ctx.h, gpu.ctypes.data, tptr.value + (off // C) * 32, nb * 32, 2))
+            same = same and bool(np.array_equal(out[:nb * 32], gpu[:nb * 32]))
+            done += n
+            off += n
+        return done, busy, same
+
+    def oracle_encode(b0, n, nb):
+        rc = O.encode_raw(p, S, fk, ak, host.ctypes.data, n, b0, nb, out.ctypes.data, threads, cxx)
         if rc:
             raise RuntimeError("oracle error %d" % rc)
-        done += n
-        off += n
-    res = {"value": round(done / GIB / busy, 4), "unit": "GiB/s", "cores": threads,
-           "kind": "port",
-           "sample": "%d MiB prefix of the same synthetic file (%d blocks), oracle/swizzle_oracle.c "
-                     "(%s), %d pthreads, %.1f s" % (
-                         done >> 20, done // C,
-                         "cxx prf: OpenSSL AES-NI CFB-128 + BIGNUM" if cxx else
-                         "OpenSSL AES-NI CFB8 + BIGNUM", threads, busy),
-           "host": info}
+
+    oracle_budget = seconds if cxx else max(2.0, seconds / 3)
+    done, busy, same = timed(oracle_encode, oracle_budget)
+    oracle_row = {"value": round(done / GIB / busy, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+                  "sample": "%d MiB prefix of the same synthetic file (%d blocks), oracle/swizzle_oracle.c "
+                            "(%s), %d pthreads, %.1f s" % (
+                                done // (1 << 20), done // C,
+                                "cxx prf: OpenSSL AES-NI CFB-128 + BIGNUM" if cxx else
+                                "OpenSSL AES-NI CFB8 + BIGNUM", threads, busy),
+                  "tags_equal_gpu": same}
     if cxx:
-        return res
+        return dict(oracle_row, host=info)
+    from baseline import cpu as NC
+    aesni = bool(NC.lib().hbcpu_aesni())
+
+    def native_encode(b0, n, nb):
+        NC.encode_raw(p, S, fk, ak, host.ctypes.data, n, b0, nb, out.ctypes.data, threads)
+
+    native_encode(0, min(piece, length), min(piece, length) // C)      # warm-up (page faults, threads)
+    done, busy, same = timed(native_encode, seconds)
+    res = {"value": round(done / GIB / busy, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+           "name": "cxx Swizzle counterpart: native C++ encoder (BASELINE.md 3)",
+           "sample": "%d MiB prefix of the same synthetic file (%d blocks), baseline/hb_cpu_swizzle.cpp "
+                     "(%s, SHA-NI SHA256_Transform, 64-bit-limb Montgomery MAC), %d std::threads, %.1f s" % (
+                         done // (1 << 20), done // C,
+                         "AES-NI, 8 evaluations interleaved per thread" if aesni else "portable byte AES",
+                         threads, busy),
+           "tags_equal_gpu": same,
+           "oracle_row": oracle_row,
+           "host": info}
     # the "PySwizzle" row: pure Python, one core, the reference's algorithmic cost
     from oracle import pyswizzle_port as PP
     rows = []
