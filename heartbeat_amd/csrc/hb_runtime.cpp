@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hbswizzle.h"
@@ -57,6 +58,26 @@ struct DevBuf {
     }
 };
 
+// Pinned host buffer (hipHostMalloc): async H2D staging.
+struct HostBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= n) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipHostMalloc(&p, want ? want : 1, 0);
+        if (e == hipSuccess) n = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
 }  // namespace
 
 struct hb_ctx {
@@ -72,6 +93,7 @@ struct hb_ctx {
     DevBuf afrag;        // MFMA MAC: digit fragments of alpha_j R mod p
     DevBuf ctl;          // wsum column counters + flags (zero between operations)
     DevBuf mseeds, moffs, mdig;   // Merkle chunk seeds, offsets, HMAC digests
+    HostBuf gstage[2];   // host-file prove: pinned gather buffers (blocks | tags), double-buffered
     bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
     u32 *hres = nullptr; // pinned host copy of wsum results (+ status)
     size_t hres_n = 0;
@@ -632,6 +654,19 @@ struct Gather {
     u32 ss, S, tw;
     bool wrap32;
     const uint8_t *tags;
+    // Indices [0, n) over `threads` host threads (contiguous slices): the
+    // gather is random reads of a (mapped) file, bound by page-cache / DRAM
+    // latency per block, so it scales with threads.
+    void run_parallel(const u64 *idx, u64 n, uint8_t *blocks, uint8_t *gtags, int threads) const {
+        const u64 T = threads < 2 || n < 2048 ? 1 : (u64)threads;
+        if (T == 1) return run(idx, n, blocks, gtags);
+        std::vector<std::thread> ts;
+        for (u64 t = 0; t < T; ++t) {
+            const u64 a = n * t / T, b = n * (t + 1) / T;
+            ts.emplace_back([=] { run(idx + a, b - a, blocks + a * C, gtags + a * tw); });
+        }
+        for (auto &th : ts) th.join();
+    }
     void run(const u64 *idx, u64 n, uint8_t *blocks, uint8_t *gtags) const {
         for (u64 i = 0; i < n; ++i) {
             const u64 ix = idx[i];
@@ -651,6 +686,17 @@ struct Gather {
         }
     }
 };
+
+// Host threads for the host-file prove gather: $HB_GATHER_THREADS, else
+// the process's CPU share ($OMP_NUM_THREADS, as GPU boxes export it) capped
+// at 16.
+int gather_threads() {
+    const char *e = getenv("HB_GATHER_THREADS");
+    if (!e || !*e) e = getenv("OMP_NUM_THREADS");
+    int t = e && *e ? atoi(e) : (int)std::thread::hardware_concurrency();
+    if (t < 1) t = 1;
+    return t > 16 ? 16 : t;
+}
 
 template <int NL>
 int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
@@ -782,27 +828,40 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         for (u64 i = 0; i < n; ++i)
             if (hidx[(size_t)i] >= ntags) hidx[(size_t)i] = 0;
         Gather G{data, len, C, pi.ss, S, pi.tw, cxx, htags};
+        // batches of <= 256 MiB, gathered by host threads into pinned buffer
+        // s = k % 2 while the GPU copies and sums batch k - 1 from the other
+        // one (same stream: H2D(k) then wsum(k), in order)
         const u64 per = (u64)((256ull << 20) / (C + pi.tw)) ? (256ull << 20) / (C + pi.tw) : 1;
         const u64 bn = n < per ? n : per;
-        HB_CHECK(c->data[0].ensure((size_t)(bn * C)), "hipMalloc(staging)");
-        HB_CHECK(c->gtags.ensure((size_t)(bn * pi.tw)), "hipMalloc(staging)");
-        std::vector<uint8_t> gblocks((size_t)(bn * C)), gtags((size_t)(bn * pi.tw));
-        for (u64 b0 = 0; b0 < n; b0 += bn) {
+        const size_t stage = (size_t)(bn * C + bn * pi.tw);
+        const int nbuf = n > bn ? 2 : 1;
+        for (int s = 0; s < nbuf; ++s) {
+            HB_CHECK(c->gstage[s].ensure(stage), "hipHostMalloc(staging)");
+            HB_CHECK(c->data[s].ensure(stage), "hipMalloc(staging)");
+        }
+        const int threads = gather_threads();
+        u64 k = 0;
+        for (u64 b0 = 0; b0 < n; b0 += bn, ++k) {
             const u64 m = n - b0 < bn ? n - b0 : bn;
-            // previous batch's kernel reads the staging buffers: wait for it
-            if (b0) HB_CHECK(hipStreamSynchronize(c->stream), "prove batch");
-            G.run(&hidx[(size_t)b0], m, gblocks.data(), gtags.data());
-            HB_CHECK(hipMemcpyAsync(c->data[0].p, gblocks.data(), (size_t)(m * C), hipMemcpyHostToDevice, c->stream), "H2D");
-            HB_CHECK(hipMemcpyAsync(c->gtags.p, gtags.data(), (size_t)(m * pi.tw), hipMemcpyHostToDevice, c->stream), "H2D");
+            const int s = (int)(k % 2);
+            // batch k - 2's H2D from this pinned buffer must have completed
+            if (k >= 2) HB_CHECK(hipEventSynchronize(c->copied[s]), "prove batch");
+            uint8_t *hb = (uint8_t *)c->gstage[s].p;
+            G.run_parallel(&hidx[(size_t)b0], m, hb, hb + bn * C, threads);
+            uint8_t *db = (uint8_t *)c->data[s].p;
+            HB_CHECK(hipMemcpyAsync(db, hb, (size_t)(m * C), hipMemcpyHostToDevice, c->stream), "H2D");
+            HB_CHECK(hipMemcpyAsync(db + bn * C, hb + bn * C, (size_t)(m * pi.tw), hipMemcpyHostToDevice, c->stream),
+                     "H2D");
+            HB_CHECK(hipEventRecord(c->copied[s], c->stream), "hipEventRecord");
             A.mode = 2;
             A.w = (const u32 *)c->wts.p + b0 * NL;
             A.nterms = m;
-            A.data = (const unsigned char *)c->data[0].p;
+            A.data = db;
             A.len = m * C;
-            A.tags = (const unsigned char *)c->gtags.p;
+            A.tags = db + bn * C;
             A.accumulate = b0 ? 1u : 0u;
             A.finalize = b0 + m == n ? 1u : 0u;
-            rc = launch_wsum<NL>(c, A, full16(pi, NL, C, c->data[0].p) ? 16 : 1);
+            rc = launch_wsum<NL>(c, A, full16(pi, NL, C, db) ? 16 : 1);
             if (rc) return rc;
             c->last_launches++;
         }
@@ -976,6 +1035,8 @@ void hb_ctx_destroy(hb_ctx *c) {
                       &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig};
     for (DevBuf *b : bufs) b->release();
     if (c->hres) (void)hipHostFree(c->hres);
+    c->gstage[0].release();
+    c->gstage[1].release();
     if (c->t0) (void)hipFree(c->t0);
     if (c->queue) (void)hipFree(c->queue);
     if (c->k0) (void)hipEventDestroy(c->k0);
