@@ -347,7 +347,8 @@ def bench_encode(args, cfg, R):
             rec = json.load(open(prof)).get(args.config + ("_cxx" if cxx else ""))
             if rec and rec.get("file_bytes") == length and len(pieces) == 1:
                 traffic = rec["hbm_bytes_per_launch"]
-                pmc = {k: rec[k] for k in ("valu_busy", "lds_busy", "source_valu") if k in rec} or None
+                pmc = {k: rec[k] for k in ("lds_busy", "held_clock_ghz", "valu_wave_instr_per_cu_clk", "source_pmc")
+                       if k in rec} or None
         except (ValueError, KeyError):
             traffic = None
 
@@ -402,10 +403,12 @@ def bench_encode(args, cfg, R):
             "kernel_ms": round(kernel_ms, 3),
             "algorithmic_bytes_per_launch": length,
             "binding_resource": {
-                "resource": "LDS ds_read_b32 T-table lookups (VALU issue co-binding, DESIGN.md 5.1)",
+                "resource": "LDS ds_read_b32 T-table lookups at the power-limited held clock (DESIGN.md 5.1)",
                 "achieved_per_s": lds_rate,
                 "peak_per_s": lds_peak,
                 "frac": round(lds_rate / lds_peak, 4),
+                "frac_at_held_clock": round(lds_rate / (lds_peak / CLOCK_GHZ * pmc["held_clock_ghz"]), 4)
+                if pmc and pmc.get("held_clock_ghz") else None,
                 "pmc": pmc,
             },
         },

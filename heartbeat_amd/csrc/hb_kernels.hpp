@@ -508,7 +508,12 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
             hb_i32x4 b[HB_MFMA_BATCH];
 #pragma unroll
             for (int jj = 0; jj < HB_MFMA_BATCH; ++jj)
+#if defined(HB_EXP_MFMA_NOLOAD)   // phase-cost experiment only (wrong tags): no sector loads
+                (void)ok; (void)src;
+                b[jj] = hb_i32x4{(int32_t)jb, (int32_t)(j0 + jj), 1, 2};
+#else
                 b[jj] = ok && j0 + jj < S ? src[2 * (j0 + jj)] : hb_i32x4{0, 0, 0, 0};
+#endif
 #pragma unroll
             for (int jj = 0; jj < HB_MFMA_BATCH; ++jj) {
                 // past the last sector: a zero B (after the -128 shift) against

@@ -39,7 +39,8 @@ typedef uint64_t u64;
 // build (hb_build_flags), so heartbeat_amd refuses it unless HB_LIB_PATH
 // selects it explicitly.
 #if (defined(HB_EXP_NO_SHA) || defined(HB_EXP_MAC_NOLOAD) || defined(HB_EXP_NO_MAC) || \
-     defined(HB_EXP_NO_FINISH) || defined(HB_EXP_NO_MFMA)) && !defined(HB_EXPERIMENT_BUILD)
+     defined(HB_EXP_NO_FINISH) || defined(HB_EXP_NO_MFMA) || defined(HB_EXP_MFMA_NOLOAD)) && \
+    !defined(HB_EXPERIMENT_BUILD)
 #error "HB_EXP_* switches produce wrong tags: experiment builds only (scripts/build_variant.sh)"
 #endif
 

@@ -16,7 +16,8 @@ for round in $(seq ${ROUNDS:-2}); do
   for v in ${VARIANTS:-base}; do
     r=$((r+1))
     if [ "$v" = base ]; then unset HB_LIB_PATH; else export HB_LIB_PATH=$PWD/exp_$v.so; fi
-    step c3_${v}_$round 300 python -u bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-parity-sample ${BENCHARGS} || exit 1
+    ps="--no-parity-sample"; [ -n "$PARITY" ] && [ $round = 1 ] && ps=""
+    step c3_${v}_$round 300 python -u bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline $ps ${BENCHARGS} || exit 1
   done
 done
 unset HB_LIB_PATH

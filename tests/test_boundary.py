@@ -172,7 +172,7 @@ def test_product_build_is_not_an_experiment_build():
     assert _native.lib().hb_build_flags() & _native.HB_BUILD_EXPERIMENT == 0
     csrc = os.path.join(ROOT, "heartbeat_amd", "csrc")
     src = '#include "hb_lane.hpp"\nint main() { return 0; }\n'
-    for flag in ("-DHB_EXP_NO_MAC", "-DHB_EXP_NO_SHA", "-DHB_EXP_MAC_NOLOAD"):
+    for flag in ("-DHB_EXP_NO_MAC", "-DHB_EXP_NO_SHA", "-DHB_EXP_MAC_NOLOAD", "-DHB_EXP_MFMA_NOLOAD"):
         r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++", "-I", csrc, flag, "-"],
                            input=src.encode(), capture_output=True)
         assert r.returncode != 0 and b"experiment builds only" in r.stderr, flag
