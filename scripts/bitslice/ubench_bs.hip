@@ -125,6 +125,9 @@ static const int kCheckBlocks = 64 * 32;   // 64 quads x 32 evaluations
 
 template <int WG, int NT, int OCC, int TPRIO = 0>
 static void run(const char *name, Args &A, Args *dA, int grid, int ncu, double clk_ghz) {
+    // HB_BS_ONLY: run only the configurations whose name contains it
+    const char *only = getenv("HB_BS_ONLY");
+    if (only && !strstr(name, only)) return;
     CK(hipMemset(A.count, 0, 16));
     hipLaunchKernelGGL((kmix<WG, NT, OCC, TPRIO>), dim3(grid), dim3(WG), 0, 0, A);
     CK(hipDeviceSynchronize());
@@ -192,6 +195,8 @@ int main(int argc, char **argv) {
 
     // ---- throughput: 0.2 s per configuration
     A.ticks = 20000000ull;
+    // HB_BS_SECONDS: longer runs per configuration (power sampling)
+    if (getenv("HB_BS_SECONDS")) A.ticks = (unsigned long long)(atof(getenv("HB_BS_SECONDS")) * 1e8);
     run<256, 0, 1>("bitsliced 4 waves/CU", A, nullptr, ncu, ncu, clk_ghz);
     run<256, 0, 2>("bitsliced 8 waves/CU", A, nullptr, 2 * ncu, ncu, clk_ghz);
     run<256, 0, 3>("bitsliced 12 waves/CU", A, nullptr, 3 * ncu, ncu, clk_ghz);
