@@ -336,6 +336,10 @@ def bench_encode(args, cfg, R):
             # built once per step (2^24 + 2^16 + 2^8 byte-0 AES) per piece
             aes += len(pieces) * ((1 << 24) + (1 << 16) + (1 << 8)) - 4 * nblocks
         lookups = aes * (16 * 12 + 5)
+        if not args.single_pass:
+            # a first try's steps 4-7 skip the round-1 lookups of the register's
+            # zero words (hb_lane.hpp, hb_aes_round1_z): 12 + 3 * 8 per block
+            lookups -= 36 * nblocks
     lds_rate = lookups / (kernel_ms * 1e-3)
     lds_peak = NUM_CUS * CLOCK_GHZ * 1e9 * LDS_LOOKUPS_PER_CLK_CU
 

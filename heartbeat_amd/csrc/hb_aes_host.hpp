@@ -94,6 +94,26 @@ inline bool aes_expand(const uint8_t *key, size_t key_len, AesKey &k) {
     return true;
 }
 
+// Round-1 constants of CFB-8 steps whose register starts with z = 1..3 zero
+// words (device: hb_aes_round1_z, PrfParams::r1z): for z and output column c,
+// round key 1 word c XOR the T-table lookups of column c that read a word
+// w_j = rk[j], j < z (column c reads byte r of word (c + r) mod 4 through
+// T_r = rotl(T0, 8 r)).
+inline void aes_round1_zero_consts(const AesKey &k, uint32_t out[12]) {
+    const AesTables &T = aes_tables();
+    for (int z = 1; z <= 3; ++z)
+        for (int c = 0; c < 4; ++c) {
+            uint32_t v = k.rk[4 + c];
+            for (int r = 0; r < 4; ++r) {
+                const int j = (c + r) & 3;
+                if (j >= z) continue;
+                const uint32_t t = T.t0[(k.rk[j] >> (8 * r)) & 0xffu];
+                v ^= r ? (t << (8 * r)) | (t >> (32 - 8 * r)) : t;
+            }
+            out[4 * (z - 1) + c] = v;
+        }
+}
+
 // Plain byte-oriented AES encryption of one block (host; State encryption only).
 inline void aes_encrypt_block(const AesKey &k, const uint8_t in[16], uint8_t out[16]) {
     const AesTables &T = aes_tables();

@@ -270,7 +270,39 @@ struct PrfParams {
     u32 R[NL];
     u32 nb;
     u32 topmask;
+    // Round-1 constants of a first try's CFB-8 steps whose shift register
+    // starts with z = 1..3 zero words (hb_aes_round1_z): r1z[4 (z - 1) + c] =
+    // round key 1 word c ^ the lookups of column c that read those words.
+    u32 r1z[12];
 };
+
+// Round 1 (hb_aes_round) when register words 0 .. z-1 are zero, z = 1..3, so
+// that w_c = rk[c] for c < z: every lookup of such a word is a constant of the
+// key, and k = r1z + 4 (z - 1) holds, per output column, round key 1 XOR those
+// constants (host: hbhost::aes_round1_zero_consts).  z is a compile-time
+// constant at every call (hb_cfb8_step's ZC).
+HB_HD void hb_aes_round1_z(const LaneTab &L, const u32 *r1z, u32 z, u32 &w0, u32 &w1, u32 &w2, u32 &w3) {
+    if (z == 3) {
+        const u32 *k = r1z + 8;
+        const u32 n0 = hb_t<3, 3>(L, w3) ^ k[0], n1 = hb_t<2, 2>(L, w3) ^ k[1];
+        const u32 n2 = hb_t<1, 1>(L, w3) ^ k[2], n3 = hb_t<0, 0>(L, w3) ^ k[3];
+        w0 = n0; w1 = n1; w2 = n2; w3 = n3;
+    } else if (z == 2) {
+        const u32 *k = r1z + 4;
+        const u32 n0 = hb_xor3(hb_t<2, 2>(L, w2), hb_t<3, 3>(L, w3), k[0]);
+        const u32 n1 = hb_xor3(hb_t<1, 1>(L, w2), hb_t<2, 2>(L, w3), k[1]);
+        const u32 n2 = hb_xor3(hb_t<0, 0>(L, w2), hb_t<1, 1>(L, w3), k[2]);
+        const u32 n3 = hb_xor3(hb_t<0, 0>(L, w3), hb_t<3, 3>(L, w2), k[3]);
+        w0 = n0; w1 = n1; w2 = n2; w3 = n3;
+    } else {
+        const u32 *k = r1z;
+        const u32 n0 = hb_xor3(hb_t<1, 1>(L, w1), hb_t<2, 2>(L, w2), hb_t<3, 3>(L, w3)) ^ k[0];
+        const u32 n1 = hb_xor3(hb_t<0, 0>(L, w1), hb_t<1, 1>(L, w2), hb_t<2, 2>(L, w3)) ^ k[1];
+        const u32 n2 = hb_xor3(hb_t<0, 0>(L, w2), hb_t<1, 1>(L, w3), hb_t<3, 3>(L, w1)) ^ k[2];
+        const u32 n3 = hb_xor3(hb_t<0, 0>(L, w3), hb_t<2, 2>(L, w1), hb_t<3, 3>(L, w2)) ^ k[3];
+        w0 = n0; w1 = n1; w2 = n2; w3 = n3;
+    }
+}
 
 // One CFB-8 step on the shift register s0..s3 (little-endian words of the 16
 // register bytes): AES it, ciphertext byte c = byte 0 of the output ^ the
@@ -279,11 +311,19 @@ struct PrfParams {
 // S[x] = byte 1 of T0[x]; XORing pk and the last round key's byte (shifted to
 // byte 1) into that word and picking its byte 1 with the same v_perm that
 // shifts s3 makes the step's bookkeeping 1 v_bitop3 + 1 v_perm + 3 v_alignbit.
-template <int NR>
-HB_HD void hb_cfb8_step(const LaneTab &L, const u32 *rk, u32 &s0, u32 &s1, u32 &s2, u32 &s3, u32 pk) {
+//
+// ZC > 0: the number of leading register words s0 .. s_{ZC-1} known to be
+// zero (only a first try's steps 4-12 have them).  Their round-1 lookups are
+// then key constants (PrfParams::r1z) and round 1 reads only the other words:
+// 4 (ZC = 3), 8 or 12 lookups instead of 16.
+template <int NR, int ZC = 0>
+HB_HD void hb_cfb8_step(const LaneTab &L, const u32 *rk, u32 &s0, u32 &s1, u32 &s2, u32 &s3, u32 pk,
+                        const u32 *r1z = nullptr) {
     u32 w0 = s0 ^ rk[0], w1 = s1 ^ rk[1], w2 = s2 ^ rk[2], w3 = s3 ^ rk[3];
+    if constexpr (ZC != 0) hb_aes_round1_z(L, r1z, ZC, w0, w1, w2, w3);
+    else hb_aes_round(L, rk + 4, w0, w1, w2, w3);
     HB_UNROLL
-    for (int r = 1; r <= NR - 2; ++r) hb_aes_round(L, rk + 4 * r, w0, w1, w2, w3);
+    for (int r = 2; r <= NR - 2; ++r) hb_aes_round(L, rk + 4 * r, w0, w1, w2, w3);
     // byte 0 of round NR-1's column 0 (the other bytes of x are not used)
     const u32 x = hb_xor3(hb_xor3(hb_t<0, 0>(L, w0), hb_t<1, 1>(L, w1), hb_t<2, 2>(L, w2)), hb_t<3, 3>(L, w3),
                           rk[4 * (NR - 1)]);
@@ -296,12 +336,15 @@ HB_HD void hb_cfb8_step(const LaneTab &L, const u32 *rk, u32 &s0, u32 &s1, u32 &
 
 // Four CFB-8 steps over the big-endian plaintext word d; returns the four
 // ciphertext bytes as a big-endian word (they are s3 afterwards, oldest lowest).
-template <int NR>
-HB_HD u32 hb_cfb8_word(const LaneTab &L, const u32 *rk, u32 &s0, u32 &s1, u32 &s2, u32 &s3, u32 d) {
-    hb_cfb8_step<NR>(L, rk, s0, s1, s2, s3, d >> 16);
-    hb_cfb8_step<NR>(L, rk, s0, s1, s2, s3, d >> 8);
-    hb_cfb8_step<NR>(L, rk, s0, s1, s2, s3, d);
-    hb_cfb8_step<NR>(L, rk, s0, s1, s2, s3, d << 8);
+// Z0 / Z1: leading zero register words before the first / the other three
+// steps (hb_cfb8_step, ZC).
+template <int NR, int Z0 = 0, int Z1 = 0>
+HB_HD u32 hb_cfb8_word(const LaneTab &L, const u32 *rk, u32 &s0, u32 &s1, u32 &s2, u32 &s3, u32 d,
+                       const u32 *r1z = nullptr) {
+    hb_cfb8_step<NR, Z0>(L, rk, s0, s1, s2, s3, d >> 16, r1z);
+    hb_cfb8_step<NR, Z1>(L, rk, s0, s1, s2, s3, d >> 8, r1z);
+    hb_cfb8_step<NR, Z1>(L, rk, s0, s1, s2, s3, d, r1z);
+    hb_cfb8_step<NR, Z1>(L, rk, s0, s1, s2, s3, d << 8, r1z);
     return hb_bswap(s3);
 }
 
@@ -325,16 +368,31 @@ HB_HD u32 hb_prf_try_from(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], c
     u32 s0 = sr[0], s1 = sr[1], s2 = sr[2], s3 = sr[3];
     // mask of the try's first output byte (the top byte of the first word)
     u32 top = FIRST ? 0xffffffffu : (P.topmask << 24) | 0xffffffu;
-    HB_NOUNROLL
-    for (u32 wi = FIRST; wi < nw; ++wi) {
-        const u32 word = hb_cfb8_word<NR>(L, P.rk, s0, s1, s2, s3, dq[0]) & top;
-        top = 0xffffffffu;
+    auto emit = [&](u32 word) {
         HB_UNROLL
         for (int t = 0; t < 7; ++t) dq[t] = dq[t + 1];
         dq[7] = 0;
         HB_UNROLL
         for (int t = NL - 1; t > 0; --t) out[t] = out[t - 1];
         out[0] = word;
+    };
+    u32 wi = FIRST;
+    // A first try enters word 1 with register words 0-2 zero (the prefix
+    // image's four steps shifted in 4 bytes): steps 4-7 start with 3, 2, 2, 2
+    // zero words, so that word is peeled with its round 1 on the key
+    // constants (36 of its 788 lookups go).  Peeling word 2 as well (steps
+    // 8-11: 2, 1, 1, 1 zero words, 20 more) measured slower (code size);
+    // word 1 alone: +0.9 % at configs[2] (same-box A/B, profiles/r03/s3).
+    if constexpr (FIRST != 0) {
+        if (wi < nw) {
+            emit(hb_cfb8_word<NR, 3, 2>(L, P.rk, s0, s1, s2, s3, dq[0], P.r1z));
+            ++wi;
+        }
+    }
+    HB_NOUNROLL
+    for (; wi < nw; ++wi) {
+        emit(hb_cfb8_word<NR>(L, P.rk, s0, s1, s2, s3, dq[0]) & top);
+        top = 0xffffffffu;
     }
     if (tail) {
         // 1-3 more bytes (nb % 4): plaintext bytes 0..tail-1 of dq[0]

@@ -146,6 +146,7 @@ bool make_prf(const uint8_t *key, size_t key_len, const uint8_t *range_be, size_
     nr = k.nr;
     memset(&P, 0, sizeof P);
     memcpy(P.rk, k.rk, sizeof(u32) * 4 * (size_t)(k.nr + 1));
+    aes_round1_zero_consts(k, P.r1z);
     Limbs R = from_be(range_be, range_len, NL);
     for (int t = 0; t < NL; ++t) P.R[t] = R[t];
     int bits = bitlen_be(range_be, range_len);

@@ -45,6 +45,7 @@ static bool make_prf(const uint8_t *key, size_t keylen, const uint8_t *range_be,
     nr = k.nr;
     memset(&P, 0, sizeof P);
     memcpy(P.rk, k.rk, sizeof(uint32_t) * 4 * (k.nr + 1));
+    aes_round1_zero_consts(k, P.r1z);
     Limbs R = from_be(range_be, rlen, NL);
     for (int t = 0; t < NL; ++t) P.R[t] = R[t];
     int bits = bitlen_be(range_be, rlen);
