@@ -53,8 +53,12 @@ bool aes_init(const uint8_t *key, size_t len, Aes &a) {
     return true;
 }
 
+// The fast path needs AES-NI + SSE4.1 (the CFB-8 engine) and BMI2 + ADX
+// (mulx / adcx in the MAC); without any of them everything runs the portable
+// byte AES and the unsigned __int128 MAC.
 bool have_aesni() {
-    static const bool v = __builtin_cpu_supports("aes") && __builtin_cpu_supports("sse4.1");
+    static const bool v = __builtin_cpu_supports("aes") && __builtin_cpu_supports("sse4.1") &&
+                          __builtin_cpu_supports("bmi2") && __builtin_cpu_supports("adx");
     return v;
 }
 
@@ -406,6 +410,36 @@ __attribute__((target("bmi2,adx"))) void tag_block(const Job &J, const Mod<N> &M
     to_be<N>(t, tag, J.tw);
 }
 
+// The same tag without BMI2 / ADX: operand scanning in unsigned __int128.
+template <int N>
+void tag_block_portable(const Job &J, const Mod<N> &M, const std::vector<u64> &am, u64 blk, const uint8_t *F_be,
+                        u64 nbF, uint8_t *tag) {
+    u64 acc[2 * N + 1];
+    memset(acc, 0, sizeof acc);
+    u64 F[N], m[N];
+    from_be<N>(F_be, nbF, F);
+    for (int i = 0; i < N; ++i) {   // + F R
+        u64 c = F[i];
+        for (int k = N + i; c && k <= 2 * N; ++k) {
+            const u128 t = (u128)acc[k] + c;
+            acc[k] = (u64)t;
+            c = (u64)(t >> 64);
+        }
+    }
+    const u64 base = blk * J.C;
+    for (uint32_t j = 0; j < J.S; ++j) {
+        const u64 off = base + (u64)j * J.ss;
+        if (off >= J.len) break;
+        const u64 r = std::min<u64>(J.ss, J.len - off);
+        from_be<N>(J.data + off, r, m);
+        mac<N>(acc, am.data() + (size_t)j * N, m);
+        if (r != J.ss) break;
+    }
+    u64 t[N];
+    redc_reduce<N>(M, acc, t);
+    to_be<N>(t, tag, J.tw);
+}
+
 template <int N, int W>
 __attribute__((target("aes,sse4.1"))) void encode_range(const Job &J, const Prf &P, const Mod<N> &M,
                                                         const std::vector<u64> &am, u64 b0, u64 b1,
@@ -481,7 +515,7 @@ int encode_n(const uint8_t *p_be, size_t p_len, uint32_t S, const uint8_t *f_key
                     uint8_t d[32], out[512];
                     digest_decimal(block_base + b, d);
                     if (!prf_eval_portable(Pf, d, out, &tr[t])) fl[t] = 1;
-                    tag_block<N>(J, M, am, b, out, Pf.nb, tags + b * J.tw);
+                    tag_block_portable<N>(J, M, am, b, out, Pf.nb, tags + b * J.tw);
                 }
             }
         });
@@ -495,6 +529,136 @@ int encode_n(const uint8_t *p_be, size_t p_len, uint32_t S, const uint8_t *f_key
     }
     if (tries_out) *tries_out = sum;
     return f ? -3 : 0;
+}
+
+// ------------------------------------------------------------------ prove
+// KeyedPRF(P)(x0 + k) for k < n, nb big-endian bytes each: the encode's
+// interleaved AES-NI engine (W evaluations per thread, re-dealt per try).
+template <int W>
+__attribute__((target("aes,sse4.1"))) void prf_range_ni(const Prf &P, u64 x0, u64 n, uint8_t *out, int *fail) {
+    Lanes<W> L;
+    u64 next = 0;
+    auto load = [&](int l) {
+        L.active[l] = next < n;
+        L.reg[l] = _mm_setzero_si128();
+        L.tries[l] = 0;
+        if (!L.active[l]) return;
+        L.job[l] = next++;
+        uint8_t d[32];
+        digest_decimal(x0 + L.job[l], d);
+        memset(L.pt[l], 0, P.nb);
+        memcpy(L.pt[l], d, std::min<u64>(32, P.nb));
+    };
+    for (int l = 0; l < W; ++l) load(l);
+    for (;;) {
+        bool any = false;
+        for (int l = 0; l < W; ++l) any |= L.active[l];
+        if (!any) break;
+        const unsigned acc = prf_try<W>(P, L);
+        for (int l = 0; l < W; ++l) {
+            if (!L.active[l]) continue;
+            if (acc >> l & 1) {
+                memcpy(out + L.job[l] * P.nb, L.out[l], P.nb);
+                load(l);
+            } else if (L.tries[l] >= 4096) {
+                *fail = 1;
+                L.active[l] = false;
+            }
+        }
+    }
+}
+
+void prf_range(const Prf &P, u64 x0, u64 n, uint8_t *out, int *fail) {
+    if (have_aesni()) return prf_range_ni<8>(P, x0, n, out, fail);
+    u64 tr = 0;
+    for (u64 k = 0; k < n; ++k) {
+        uint8_t d[32];
+        digest_decimal(x0 + k, d);
+        if (!prf_eval_portable(P, d, out + k * P.nb, &tr)) *fail = 1;
+    }
+}
+
+// acc (2N + 1 limbs) -> acc mod p: REDC gives acc R^-1 mod p, one more
+// Montgomery multiplication by R^2 gives acc mod p.
+template <int N>
+void acc_mod(const Mod<N> &M, u64 *acc, u64 *out) {
+    u64 t[N];
+    redc_reduce<N>(M, acc, t);
+    to_mont<N>(M, t, out);
+}
+
+// PySwizzle.prove (heartbeat/PySwizzle/PySwizzle.py:333-370): idx_i =
+// KeyedPRF(key, ntags)(i), v_i = KeyedPRF(key, v_max)(i); mu_j = sum_i v_i
+// m_{idx_i, j} mod p (sector j of block idx_i read at idx_i C + j ss, a short
+// read counts as its bytes and ends the block), sigma = sum_i v_i tag[idx_i]
+// mod p.  The reference's native loop is cxx/shacham_waters_private.cxx:731-789.
+// Threads take contiguous slices of the challenge; every sum stays exact in
+// 2N + 1 limbs until the end.
+template <int N>
+int prove_n(const uint8_t *p_be, size_t p_len, uint32_t S, const uint8_t *key, size_t key_len, u64 chunks,
+            const uint8_t *vmax_be, size_t vmax_len, u64 ntags, const uint8_t *tags, const uint8_t *data, u64 len,
+            int threads, uint8_t *mu_out, uint8_t *sigma_out) {
+    Mod<N> M;
+    mod_init<N>(p_be, p_len, M);
+    const int bits = bitlen_be(p_be, p_len);
+    const u64 ss = (u64)bits / 8, tw = (u64)(bits + 7) / 8, C = ss * S;
+    if (bitlen_be(vmax_be, vmax_len) > 64 * N) return -4;
+    uint8_t nbe[8];
+    for (int k = 0; k < 8; ++k) nbe[k] = (uint8_t)(ntags >> (56 - 8 * k));
+    Prf Pi, Pv;
+    if (!prf_init(key, key_len, nbe, 8, Pi) || !prf_init(key, key_len, vmax_be, vmax_len, Pv)) return -1;
+    threads = std::max(1, threads);
+    const u64 T = std::min<u64>((u64)threads, std::max<u64>(1, chunks / 64));
+    const size_t W = 2 * N + 1;
+    std::vector<u64> accs((size_t)T * (S + 1) * W, 0);
+    std::vector<int> fl(T, 0);
+    std::vector<std::thread> ts;
+    for (u64 t = 0; t < T; ++t) {
+        ts.emplace_back([&, t] {
+            const u64 i0 = chunks * t / T, i1 = chunks * (t + 1) / T, n = i1 - i0;
+            std::vector<uint8_t> ib((size_t)n * Pi.nb), vb((size_t)n * Pv.nb);
+            prf_range(Pi, i0, n, ib.data(), &fl[t]);
+            prf_range(Pv, i0, n, vb.data(), &fl[t]);
+            u64 *acc = &accs[(size_t)t * (S + 1) * W];
+            u64 v[N], m[N];
+            for (u64 k = 0; k < n; ++k) {
+                u64 ix = 0;
+                for (u64 b = 0; b < Pi.nb; ++b) ix = (ix << 8) | ib[(size_t)(k * Pi.nb + b)];
+                from_be<N>(&vb[(size_t)(k * Pv.nb)], Pv.nb, v);
+                const u64 base = ix * C;
+                for (uint32_t j = 0; j < S; ++j) {
+                    const u64 off = base + (u64)j * ss;
+                    if (off >= len) break;
+                    const u64 r = std::min<u64>(ss, len - off);
+                    from_be<N>(data + off, r, m);
+                    mac<N>(acc + (size_t)j * W, v, m);
+                    if (r != ss) break;
+                }
+                from_be<N>(tags + ix * tw, tw, m);
+                mac<N>(acc + (size_t)S * W, v, m);
+            }
+        });
+    }
+    for (auto &th : ts) th.join();
+    for (u64 t = 0; t < T; ++t)
+        if (fl[t]) return -3;
+    for (uint32_t j = 0; j <= S; ++j) {
+        u64 sum[2 * N + 1];
+        memset(sum, 0, sizeof sum);
+        for (u64 t = 0; t < T; ++t) {
+            const u64 *a = &accs[((size_t)t * (S + 1) + j) * W];
+            u64 c = 0;
+            for (size_t k = 0; k < W; ++k) {
+                const u128 x = (u128)sum[k] + a[k] + c;
+                sum[k] = (u64)x;
+                c = (u64)(x >> 64);
+            }
+        }
+        u64 r[N];
+        acc_mod<N>(M, sum, r);
+        to_be<N>(r, j < S ? mu_out + (size_t)j * tw : sigma_out, tw);
+    }
+    return 0;
 }
 
 }  // namespace
@@ -516,6 +680,27 @@ int hbcpu_encode(const uint8_t *p_be, size_t p_len, uint32_t S, const uint8_t *f
     if (bits <= 512) return encode_n<8>(p_be, p_len, S, f_key, a_key, key_len, block_base, data, len, nblocks, tags, threads, tries_out);
     if (bits <= 1024) return encode_n<16>(p_be, p_len, S, f_key, a_key, key_len, block_base, data, len, nblocks, tags, threads, tries_out);
     if (bits <= 2048) return encode_n<32>(p_be, p_len, S, f_key, a_key, key_len, block_base, data, len, nblocks, tags, threads, tries_out);
+    return -4;
+}
+
+// PySwizzle.prove on host memory (hb_prove's contract, include/hbswizzle.h):
+// mu (S x tw bytes) and sigma (tw bytes), big-endian.  Every index must be
+// < ntags (KeyedPRF(key, ntags) guarantees it).  Returns 0, -1 (bad key /
+// prime), -3 (PRF did not terminate), -4 (prime or v_max too wide).
+int hbcpu_prove(const uint8_t *p_be, size_t p_len, uint32_t S, const uint8_t *key, size_t key_len,
+                uint64_t chunks, const uint8_t *vmax_be, size_t vmax_len, uint64_t ntags, const uint8_t *tags,
+                const uint8_t *data, uint64_t len, int threads, uint8_t *mu_out, uint8_t *sigma_out) {
+    const int bits = bitlen_be(p_be, p_len);
+    if (bits < 8 || !(p_be[p_len - 1] & 1) || ntags == 0) return -1;
+#define HB_PROVE_N(N) prove_n<N>(p_be, p_len, S, key, key_len, chunks, vmax_be, vmax_len, ntags, tags, data, len, \
+                                 threads, mu_out, sigma_out)
+    if (bits <= 64) return HB_PROVE_N(1);
+    if (bits <= 128) return HB_PROVE_N(2);
+    if (bits <= 256) return HB_PROVE_N(4);
+    if (bits <= 512) return HB_PROVE_N(8);
+    if (bits <= 1024) return HB_PROVE_N(16);
+    if (bits <= 2048) return HB_PROVE_N(32);
+#undef HB_PROVE_N
     return -4;
 }
 

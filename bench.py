@@ -83,7 +83,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: c3 (configs[2]) at --gpus 1, c4 (configs[3], 256 GiB sharded) at --gpus N > 1")
     ap.add_argument("--gib", type=float, default=None, help="override file GiB per rank")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=None,
@@ -102,7 +103,13 @@ def parse(argv=None):
                     help="also time the pinned/pageable host path on a 4 GiB prefix (DESIGN.md)")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the launch / rank / timing / JSON plumbing without HIP calls (CPU tests)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.config is None:
+        # one GPU: configs[2], the largest single-GPU configuration (the BENCH
+        # line and the N = 1 point of the scaling curve); several GPUs:
+        # configs[3], the 256 GiB file sharded over them
+        args.config = "c3" if args.gpus == 1 else "c4"
+    return args
 
 
 # ---------------------------------------------------------------- ranks
@@ -344,6 +351,7 @@ def bench_encode(args, cfg, R):
     lds_peak = NUM_CUS * CLOCK_GHZ * 1e9 * LDS_LOOKUPS_PER_CLK_CU
 
     traffic = None
+    traffic_source = None
     pmc = None
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
@@ -351,6 +359,11 @@ def bench_encode(args, cfg, R):
             rec = json.load(open(prof)).get(args.config + ("_cxx" if cxx else ""))
             if rec and rec.get("file_bytes") == length and len(pieces) == 1:
                 traffic = rec["hbm_bytes_per_launch"]
+                # not measured in this run: PMC counters cannot be read without
+                # the profiler; the committed pass of the same workload is quoted
+                traffic_source = ("profiles/pmc_traffic.json[%s]: rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE pass "
+                                  "of this workload (%s), committed; not measured in this run" % (
+                                      args.config + ("_cxx" if cxx else ""), rec.get("source_pmc", "?")))
                 pmc = {k: rec[k] for k in ("lds_busy", "held_clock_ghz", "valu_wave_instr_per_cu_clk", "source_pmc")
                        if k in rec} or None
         except (ValueError, KeyError):
@@ -394,7 +407,14 @@ def bench_encode(args, cfg, R):
             "parallelism": "dp%d block-range shards, no collective (gloo barrier + max time only)" % R.world,
         },
         "roofline": {
+            # the roofline the line is priced against (HBM bytes; the encode has
+            # no MFMA-bound phase); what actually binds it is `binding`
             "bound": "hbm",
+            "binding": "lds" if not cxx else "valu",
+            "binding_note": ("the encode is NOT HBM-bound: it is bound by LDS T-table lookups at the clock the "
+                             "socket power limit leaves (binding_resource, DESIGN.md 5.1); frac is the fraction "
+                             "of the HBM roofline it reaches") if not cxx else
+                            "cxx prf: per-block SHA-256 and the VALU MAC (DESIGN.md 5.2)",
             "achieved": round(achieved_gbs, 1),
             "peak": HBM_PEAK_GBS,
             "peak_measured": peak_measured,
@@ -402,6 +422,7 @@ def bench_encode(args, cfg, R):
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "frac_of_measured": round(achieved_gbs / peak_measured, 4) if peak_measured else None,
             "traffic": traffic,
+            "traffic_source": traffic_source,
             "kernel": "hb_cxx_encode_kernel" if cxx else "hb_encode_kernel" if args.single_pass else
                       "hb_prefix_kernel + hb_encode_first_kernel + hb_encode_retry_kernel",
             "kernel_ms": round(kernel_ms, 3),
@@ -567,8 +588,14 @@ def cpu_baseline(ctx, L, dptr, tptr, length, S, p, fk, ak, C, seconds, threads, 
 
     native_encode(0, min(piece, length), min(piece, length) // C)      # warm-up (page faults, threads)
     done, busy, same = timed(native_encode, seconds)
-    res = {"value": round(done / GIB / busy, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+    rate = done / GIB / busy
+    res = {"value": round(rate, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
            "name": "cxx Swizzle counterpart: native C++ encoder (BASELINE.md 3)",
+           "cores_available": info.get("affinity") or info.get("nproc"),
+           "per_core_gib_s": round(rate / threads, 4),
+           "cores_note": ("%d threads = this process's CPU share ($OMP_NUM_THREADS / affinity; a GPU box leases "
+                          "16 host cores per GPU and exports OMP_NUM_THREADS=16), not the whole host's %s "
+                          "CPUs; per_core_gib_s = value / cores" % (threads, info.get("affinity") or info.get("nproc"))),
            "sample": "%d MiB prefix of the same synthetic file (%d blocks), baseline/hb_cpu_swizzle.cpp "
                      "(%s, SHA-NI SHA256_Transform, 64-bit-limb Montgomery MAC), %d std::threads, %.1f s" % (
                          done // (1 << 20), done // C,
@@ -605,8 +632,51 @@ def cpu_baseline(ctx, L, dptr, tptr, length, S, p, fk, ak, C, seconds, threads, 
         dt = time.perf_counter() - t
         rows.append({"value": round(nbytes / (1 << 20) / dt, 3), "unit": "MiB/s", "cores": 1,
                      "kind": "port", "sample": "%s: %.2f MiB encoded in %.1f s" % (label, nbytes / (1 << 20), dt)})
+    rows.append(pyswizzle_test6_row())
     res["pyswizzle_rows"] = rows
     return res
+
+
+def pyswizzle_test6_row():
+    """The "PySwizzle" row on BASELINE.md 3's config 1: the reference's
+    tests/files/test6.txt (999,999 B, regenerated) at the PySwizzle defaults
+    (10 sectors, 1024-bit prime, PySwizzle.py:233), encode + prove + verify by
+    the single-core pure-Python restatement, with the keys, tags and proof of
+    the reference-generated golden case (tests/golden/file_cases.json)."""
+    import io
+    from oracle import pyswizzle_port as PP
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "file_cases.json")))
+    c = next(c for c in g["cases"] if c["name"] == "test6.txt/p1024/S10")
+    p = int(c["prime"], 16)
+    S = int(c["sectors"])
+    fk, ak = bytes.fromhex(c["f_key"]), bytes.fromhex(c["alpha_key"])
+    line = b"abcdefghijklmnopqrstuvwxyz1234567890\n"
+    data = (line * (999999 // len(line) + 1))[:999999]
+    w = (p.bit_length() + 7) // 8
+    t = time.perf_counter()
+    tags = PP.encode(p, S, fk, ak, io.BytesIO(data))
+    enc_s = time.perf_counter() - t
+    tags_ok = hashlib.sha256(b"".join(x.to_bytes(w, "big") for x in tags)).hexdigest() == c["tags_sha256"]
+    f = io.BytesIO(data)
+    ch = c["chal"]
+    ck, vmax = bytes.fromhex(ch["key"]), int(ch["v_max"], 16)
+    t = time.perf_counter()
+    mu, sg = PP.prove(p, S, f, ck, ch["chunks"], vmax, tags)
+    prove_s = time.perf_counter() - t
+    proof_ok = mu == [int(m, 16) for m in c["proof"]["mu"]] and sg == int(c["proof"]["sigma"], 16)
+    # the default challenge of gen_challenge: chunks = #tags (PySwizzle.py:329)
+    t = time.perf_counter()
+    mu2, sg2 = PP.prove(p, S, f, ck, len(tags), vmax, tags)
+    prove_all_s = time.perf_counter() - t
+    t = time.perf_counter()
+    ok = PP.verify(p, S, fk, ak, len(tags), ck, len(tags), vmax, mu2, sg2)
+    verify_s = time.perf_counter() - t
+    return {"value": round(len(data) / (1 << 20) / enc_s, 3), "unit": "MiB/s", "cores": 1, "kind": "port",
+            "sample": "test6.txt (999,999 B), 10 sectors, 1024-bit prime (PySwizzle defaults), golden keys",
+            "encode_s": round(enc_s, 3), "tags_equal_golden": tags_ok,
+            "prove_s_300_idx": round(prove_s, 3), "proof_equal_golden": proof_ok,
+            "prove_s_all_%d_idx" % len(tags): round(prove_all_s, 3),
+            "verify_s_all_idx": round(verify_s, 3), "verified": ok}
 
 
 def host_file_prove(ctx, L, dptr, pys, p, S, path, n, tag):
@@ -782,10 +852,40 @@ def bench_prove(args, cfg, R):
                 raise RuntimeError("oracle prove error %d" % rc)
             n += 1
         cpu_ms = (time.perf_counter() - t) / n * 1e3
-        line["cpu_baseline"] = {"value": round(cpu_ms, 3), "unit": "ms", "cores": 1, "kind": "port",
-                                "sample": "%d proofs of the same challenge, oracle/swizzle_oracle.c "
-                                          "(OpenSSL), 1 thread" % n}
+        oracle_row = {"value": round(cpu_ms, 3), "unit": "ms", "cores": 1, "kind": "port",
+                      "sample": "%d proofs of the same challenge, oracle/swizzle_oracle.c (OpenSSL BIGNUM), "
+                                "1 thread" % n}
         line["proof_equal_oracle"] = ref_mu.raw == mu.raw and ref_sg.raw == sg.raw
+        # the "cxx Swizzle" counterpart (idx/s prove on configs[4]):
+        # the native prove of baseline/hb_cpu_swizzle.cpp on the same host copy
+        from baseline import cpu as NC
+        info = host_cpu_info()
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or info.get("affinity") or
+                                          os.cpu_count() or 1)
+        nrow = {}
+        for th in sorted({1, threads}):
+            NC.prove_raw(p, S, ck, chunks, p, nblocks, tags.ctypes.data, host.ctypes.data, length, th)   # warm-up
+            t = time.perf_counter()
+            k = 0
+            while k < 3 or time.perf_counter() - t < min(args.cpu_seconds, 5.0):
+                nmu, nsg = NC.prove_raw(p, S, ck, chunks, p, nblocks, tags.ctypes.data, host.ctypes.data, length, th)
+                k += 1
+            nrow[th] = ((time.perf_counter() - t) / k * 1e3, k)
+        want_mu = [int.from_bytes(mu.raw[j * w:(j + 1) * w], "big") for j in range(S)]
+        ms_n, k_n = nrow[threads]
+        line["cpu_baseline"] = {
+            "value": round(ms_n, 4), "unit": "ms", "cores": threads, "kind": "port",
+            "name": "cxx Swizzle counterpart: native prove (baseline/hb_cpu_swizzle.cpp, AES-NI index/v PRFs, "
+                    "gather, 64-bit-limb MAC; reference loop cxx/shacham_waters_private.cxx:731-789)",
+            "sample": "%d proofs of the same 10,000-index challenge on the host copy of the file, %d std::threads"
+                      % (k_n, threads),
+            "idx_per_s": round(chunks / (ms_n * 1e-3), 1),
+            "one_thread_ms": round(nrow[1][0], 4),
+            "cores_available": info.get("affinity") or info.get("nproc"),
+            "proof_equal_gpu": nmu == want_mu and nsg == int.from_bytes(sg.raw, "big"),
+            "oracle_row": oracle_row,
+            "host": info}
+        line["idx_per_s"] = round(chunks / (ms * 1e-3), 1)
         del host, tags
     if R.rank == 0:
         print(json.dumps(line), flush=True)

@@ -138,7 +138,8 @@ class Context(object):
     def last_kernel_ms(self):
         ms = ctypes.c_double()
         n = ctypes.c_uint32()
-        lib().hb_last_kernel_ms(self.h, ctypes.byref(ms), ctypes.byref(n))
+        with self.lock:   # it may settle a pending async encode (hb_last_kernel_ms)
+            lib().hb_last_kernel_ms(self.h, ctypes.byref(ms), ctypes.byref(n))
         return ms.value, n.value
 
     def close(self):

@@ -489,6 +489,53 @@ __device__ __forceinline__ bool hb_block_full(const EncodeArgs<NL> &A, u64 job) 
 #define HB_MFMA_BATCH 4
 #endif
 #define HB_MFMA_LDS_S 16
+
+// x of lane (l ^ 1) / (l ^ 2) within the lane's quad (DPP quad_perm)
+__device__ __forceinline__ int32_t hb_quad_x1(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, false); }
+__device__ __forceinline__ int32_t hb_quad_x2(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xf, 0xf, false); }
+
+// Whole-line sector loads for the MFMA MAC (EncodeArgs::mfma == 2, S % 4 == 0):
+// the 4 sectors j0 .. j0+3 of the 32 blocks of group g, i.e. one 128-byte line
+// per block, as 4 loads in which each lane quad reads one contiguous 64-byte
+// half line (lane (h, 4q + i) of load r: chunk 4h + i of block 4q + r), so
+// every line is requested by ONE instruction in whole 64-byte pieces (the
+// sector-shaped loads request each line from 4 instructions, 16 bytes a lane:
+// 4x the L1 accesses and 1.4x the L1 -> L2 requests).  A 4 x 4
+// transpose inside each quad (lane bits 0-1 <-> load index, two DPP exchange
+// stages) then leaves in V[r'] at lane (h, n) chunk 4h + r' of block n: the
+// MFMA B layout, with the A fragments of slot j0 + r' built for those chunks
+// (hb_runtime.cpp, mfma_tables).
+__device__ __forceinline__ void hb_line_loads(const unsigned char *const blk[4], const bool okr[4], u32 off,
+                                              hb_i32x4 V[4]) {
+    hb_i32x4 L[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        L[r] = okr[r] ? *reinterpret_cast<const hb_i32x4 *>(blk[r] + off) : hb_i32x4{0, 0, 0, 0};
+    const u32 i = hb_lane_id() & 3u;
+    const bool b0 = i & 1u, b1 = i & 2u;
+    hb_i32x4 M[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        // stage 1: M_{r1 r0}[i1 i0] = L_{r1 i0}[i1 r0]
+        const int32_t x0 = hb_quad_x1(L[0][e]), x1 = hb_quad_x1(L[1][e]);
+        const int32_t x2 = hb_quad_x1(L[2][e]), x3 = hb_quad_x1(L[3][e]);
+        M[0][e] = b0 ? x1 : L[0][e];
+        M[1][e] = b0 ? L[1][e] : x0;
+        M[2][e] = b0 ? x3 : L[2][e];
+        M[3][e] = b0 ? L[3][e] : x2;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        // stage 2: V_{r1 r0}[i1 i0] = M_{i1 r0}[r1 i0] = L_{i1 i0}[r1 r0]
+        const int32_t y0 = hb_quad_x2(M[0][e]), y1 = hb_quad_x2(M[1][e]);
+        const int32_t y2 = hb_quad_x2(M[2][e]), y3 = hb_quad_x2(M[3][e]);
+        V[0][e] = b1 ? y2 : M[0][e];
+        V[2][e] = b1 ? M[2][e] : y0;
+        V[1][e] = b1 ? y3 : M[1][e];
+        V[3][e] = b1 ? M[3][e] : y1;
+    }
+}
+
 template <int NL, bool ALDS>
 __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const hb_i32x4 *afl, u64 job, bool active,
                                                   u32 T[2 * NL + 1]) {
@@ -499,11 +546,37 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
     long long G[2][8];   // G[g][k]: limb 2k + h of group g's column-n block
 #pragma unroll
     for (u32 g = 0; g < 2; ++g) {
+        hb_i32x16 acc0 = {}, acc1 = {};
+#if !defined(HB_NO_LINE_LOADS)
+        if (A.mfma == 2) {
+            // load r of lane (h, 4q + i) reads block 4q + r of the group (lane 32 g + 4q + r's)
+            const unsigned char *blk[4];
+            bool okr[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int src = (int)(32 * g + (n & ~3u) + r);
+                const u64 jb = (u64)__shfl((long long)job, src);
+                okr[r] = __shfl((int)mine, src) != 0;
+                blk[r] = A.data + jb * A.C + 64u * h + 16u * (l & 3u);
+            }
+            for (u32 j0 = 0; j0 < S; j0 += 4) {
+                hb_i32x4 V[4];
+                hb_line_loads(blk, okr, 32u * j0, V);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const hb_i32x4 bb = V[r] ^ (int32_t)0x80808080;
+                    const hb_i32x4 a0 = afl[(j0 + r) * 64 + l], a1 = afl[(S + j0 + r) * 64 + l];
+                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bb, acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bb, acc1, 0, 0, 0);
+                }
+            }
+        } else
+#endif
+        {
         // the block of column n in group g: lane 32 g + n's
         const u64 jb = (u64)__shfl((long long)job, (int)(32 * g + n));
         const bool ok = __shfl((int)mine, (int)(32 * g + n)) != 0;
         const hb_i32x4 *src = reinterpret_cast<const hb_i32x4 *>(A.data + jb * A.C + 16u * h);
-        hb_i32x16 acc0 = {}, acc1 = {};
         for (u32 j0 = 0; j0 < S; j0 += HB_MFMA_BATCH) {
             hb_i32x4 b[HB_MFMA_BATCH];
 #pragma unroll
@@ -525,6 +598,7 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
                 acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bb, acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bb, acc1, 0, 0, 0);
             }
+        }
         }
         // limb 8t + 2q + h of column n's block = bytes acc_t[4q .. 4q+3];
         // k = 4t + q: limb 2k + h

@@ -9,6 +9,7 @@
 // CPU compute path.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <chrono>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -307,19 +308,24 @@ u64 retry_capacity(const uint8_t *p_be, size_t p_len, u64 nb) {
 // Host-built inputs of the MFMA MAC (hb_kernels.hpp, hb_mfma_block_acc) from
 // alpha_j R mod p (c->alpha_mont, on the device): the A-operand fragments of
 // the signed base-256 digit Toeplitz matrices and kz.
-int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17]) {
+// Layouts: 1 = sector loads (slot j holds sector j: lane (h, m) byte e is
+// byte 16 h + e of sector j); 2 = whole-line loads (S % 4 == 0; slot j0 + r,
+// j0 % 4 == 0, holds chunk 4h + r of the line of sectors j0 .. j0+3: byte
+// 16 (r % 2) + e of sector j0 + 2h + r / 2), see hb_line_loads.
+int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
     const int NL = 8;
     std::vector<u32> am((size_t)S * NL);
     HB_CHECK(hipMemcpyAsync(am.data(), c->alpha_mont.p, am.size() * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
     HB_CHECK(hipStreamSynchronize(c->stream), "alpha PRF");
     std::vector<int8_t> frag((size_t)2 * S * 64 * 16);
+    std::vector<int> digits((size_t)S * 33);
     Limbs sum(NL, 0);
     for (u32 j = 0; j < S; ++j) {
         const u32 *a = &am[(size_t)j * NL];
         Limbs aj(a, a + NL);
         sum = add_mod(sum, aj, p);
         // balanced base-256 digits: alpha = sum_i d_i 256^i, d_i in [-128, 127], i <= 32
-        int d[33];
+        int *d = &digits[(size_t)j * 33];
         int carry = 0;
         for (int i = 0; i < 32; ++i) {
             int x = (int)((a[i / 4] >> (8 * (i % 4))) & 0xffu) + carry;
@@ -327,13 +333,26 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17]) {
             d[i] = x - 256 * carry;
         }
         d[32] = carry;
+    }
+    for (u32 slot = 0; slot < S; ++slot)
         for (int t = 0; t < 2; ++t)
             for (int l = 0; l < 64; ++l)
                 for (int e = 0; e < 16; ++e) {
-                    const int col = 32 * t + (l & 31), k = 16 * (l >> 5) + e, i = col - 31 + k;
-                    frag[(((size_t)t * S + j) * 64 + l) * 16 + e] = (int8_t)(i >= 0 && i <= 32 ? d[i] : 0);
+                    const int h = l >> 5;
+                    u32 j;
+                    int k;   // byte of sector j (weight 256^(31 - k))
+                    if (layout == 2) {
+                        const u32 r = slot & 3u;
+                        j = (slot & ~3u) + 2u * (u32)h + r / 2u;
+                        k = 16 * (int)(r & 1u) + e;
+                    } else {
+                        j = slot;
+                        k = 16 * h + e;
+                    }
+                    const int col = 32 * t + (l & 31), i = col - 31 + k;
+                    const int *d = &digits[(size_t)j * 33];
+                    frag[(((size_t)t * S + slot) * 64 + l) * 16 + e] = (int8_t)(i >= 0 && i <= 32 ? d[i] : 0);
                 }
-    }
     // Q = 0x80..80 (32 bytes): sum_j alpha_j u_j = sum_j alpha_j (u_j - Q) + Q sum_j alpha_j
     Limbs q(NL, 0x80808080u);
     Limbs k = mul_mod(mod_any(q, p), sum, p);
@@ -391,6 +410,16 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
                 const uint8_t *data, u64 len, u64 nblocks, uint8_t *tags, u32 flags, u64 *tries_out) {
     Limbs p = from_be(p_be, p_len, NL);
     const u64 C = (u64)pi.ss * S;
+    // $HB_TRACE_PHASES: host-side phase times of this call on stderr (the
+    // stream is synchronized at each mark; diagnosis of first-call costs)
+    static const bool trace = getenv("HB_TRACE_PHASES") != nullptr;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (!trace) return;
+        (void)hipStreamSynchronize(c->stream);
+        fprintf(stderr, "[hb_encode] %-28s %9.3f ms\n", what,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+    };
     // alpha_j R mod p, j < S  (alpha = KeyedPRF(alpha_key, p), PySwizzle.py:291,302)
     HB_CHECK(c->alpha_raw.ensure((size_t)S * NL * 4), "hipMalloc");
     HB_CHECK(c->alpha_mont.ensure((size_t)S * NL * 4), "hipMalloc");
@@ -401,6 +430,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     if (rc) return rc;
     rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S);
     if (rc) return rc;
+    mark("alpha PRF + Montgomery");
 
     EncodeArgs<NL> A;
     memset(&A, 0, sizeof A);
@@ -411,12 +441,20 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         // phase's fixed cost: measured 67.2 vs 72.7 GiB/s at configs[1], S = 1)
         if (!cxx && pi.ss == 32 && S >= 4 && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
             !getenv("HB_NO_MFMA")) {
-            rc = mfma_tables(c, p, S, A.kz);
+            // whole-line sector loads when every line of 4 sectors lies in
+            // one block ($HB_MFMA_SECTOR_LOADS: the sector-shaped loads, A/B)
+#if defined(HB_NO_LINE_LOADS)
+            const int layout = 1;
+#else
+            const int layout = S % 4 == 0 && !getenv("HB_MFMA_SECTOR_LOADS") ? 2 : 1;
+#endif
+            rc = mfma_tables(c, p, S, A.kz, layout);
             if (rc) return rc;
-            A.mfma = 1;
+            A.mfma = (u32)layout;
             A.afrag = (const u32 *)c->afrag.p;
         }
     }
+    mark("MFMA tables");
     int nr = 0;
     if (!make_prf<NL>(f_key, key_len, p_be, p_len, A.prf, nr)) return fail(c, HB_EINVAL, "invalid key");
     make_mod<NL>(p, A.mod);
@@ -451,6 +489,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(c->retry.ensure((size_t)(A.retry_cap ? A.retry_cap : 1) * sizeof(HbRetry)), "hipMalloc(retry)");
         A.retry = (HbRetry *)c->retry.p;
         A.retry_count = q0 + 3;
+        mark("retry list");
     }
     if (two_pass && !cxx) {
         HB_CHECK(c->pfx.ensure(HB_PFX_BYTES), "hipMalloc(prefix)");
@@ -460,6 +499,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         uint8_t zero[16] = {0}, o[16];
         aes_encrypt_block(k, zero, o);
         A.o0 = o[0];
+        mark("prefix image buffer");
     }
     c->last_launches = 0;
     float ms_total = 0.f;
@@ -516,6 +556,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         }
         HB_CHECK(hipEventSynchronize(c->k1), "encode");
         HB_CHECK(hipEventElapsedTime(&ms_total, c->k0, c->k1), "hipEventElapsedTime");
+        mark("kernels");
     } else {
         // Host bytes: chunks of whole blocks double-buffered through the GPU,
         // H2D on the copy stream overlapping the encode kernels of the previous
@@ -809,7 +850,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         c->last_launches++;
     } else {
         // Host bytes: the challenged blocks are gathered on the host -- the
-        // reference's seek/read per index -- in batches of <= 256 MiB staged
+        // reference's seek/read per index -- in batches of <= 64 MiB staged
         // through the GPU; each batch adds onto the running sums.
         std::vector<u64> hidx((size_t)n);
         if (check_all) {
@@ -829,10 +870,17 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         for (u64 i = 0; i < n; ++i)
             if (hidx[(size_t)i] >= ntags) hidx[(size_t)i] = 0;
         Gather G{data, len, C, pi.ss, S, pi.tw, cxx, htags};
-        // batches of <= 256 MiB, gathered by host threads into pinned buffer
+        // batches of <= 64 MiB, gathered by host threads into pinned buffer
         // s = k % 2 while the GPU copies and sums batch k - 1 from the other
         // one (same stream: H2D(k) then wsum(k), in order)
-        const u64 per = (u64)((256ull << 20) / (C + pi.tw)) ? (256ull << 20) / (C + pi.tw) : 1;
+        // 64 MiB batches: the two pinned buffers stay with the context (128 MiB
+        // of page-locked host memory per context until hb_ctx_destroy)
+        u64 per = (u64)((64ull << 20) / (C + pi.tw)) ? (64ull << 20) / (C + pi.tw) : 1;
+        // test hook: smaller batches, to exercise the double buffering
+        if (const char *t = getenv("HB_TEST_PROVE_BATCH")) {
+            const u64 cap = (u64)strtoull(t, nullptr, 10);
+            if (cap >= 1 && cap < per) per = cap;
+        }
         const u64 bn = n < per ? n : per;
         const size_t stage = (size_t)(bn * C + bn * pi.tw);
         const int nbuf = n > bn ? 2 : 1;
@@ -1322,14 +1370,12 @@ int hb_aes_cfb128(const uint8_t *key, size_t key_len, const uint8_t *iv, const u
     return 0;
 }
 
-int hb_last_kernel_ms(const hb_ctx *c, double *ms, uint32_t *launches) {
+int hb_last_kernel_ms(hb_ctx *c, double *ms, uint32_t *launches) {
     if (!c) return HB_EINVAL;
     // a pending HB_ASYNC encode is the last one: complete it first (its status
-    // stays for hb_ctx_wait)
-    if (c->pending) {
-        hb_ctx *m = const_cast<hb_ctx *>(c);
-        if (hipSetDevice(m->device) == hipSuccess) settle(m);
-    }
+    // stays for hb_ctx_wait); like every call on a context, not concurrently
+    // with another call on the same context
+    if (c->pending && hipSetDevice(c->device) == hipSuccess) settle(c);
     if (ms) *ms = c->last_ms;
     if (launches) *launches = c->last_launches;
     return 0;

@@ -253,7 +253,7 @@ int hb_aes_cfb128(const uint8_t *key, size_t key_len, const uint8_t *iv,
  * the encode kernel (HIP events on the kernel's stream), and launch count.  A
  * pending HB_ASYNC encode is completed first (its status stays for
  * hb_ctx_wait). */
-int hb_last_kernel_ms(const hb_ctx *ctx, double *ms, uint32_t *launches);
+int hb_last_kernel_ms(hb_ctx *ctx, double *ms, uint32_t *launches);
 
 /* Device memory helpers so that callers without a GPU framework (e.g. a cgo or
  * JNI binding) can hold a device-resident file: allocate, copy

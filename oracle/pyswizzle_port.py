@@ -113,3 +113,44 @@ def encode(p, sectors, f_key, alpha_key, file):
         sigmas.append(sigma)
         chunk_id += 1
     return sigmas
+
+
+def prove(p, sectors, file, chal_key, chunks, v_max, tags):
+    """PySwizzle.prove's loops (PySwizzle.py:333-370): (mu list, sigma).  Like
+    the reference, index.eval(i) and v.eval(i) are recomputed for every sector
+    and again for sigma, and the file is read by seek/read per sector."""
+    sectorsize = p.bit_length() // 8
+    chunk_size = sectors * sectorsize
+    index = KeyedPRF(chal_key, len(tags))
+    v = KeyedPRF(chal_key, v_max)
+    mu = [0] * sectors
+    sigma = 0
+    for i in range(0, chunks):
+        for j in range(0, sectors):
+            pos = index.eval(i) * chunk_size + j * sectorsize
+            file.seek(pos)
+            buffer = file.read(sectorsize)
+            if len(buffer) > 0:
+                mu[j] += v.eval(i) * int.from_bytes(buffer, "big")
+            if len(buffer) != sectorsize:
+                break
+    for j in range(0, sectors):
+        mu[j] %= p
+    for i in range(0, chunks):
+        sigma += v.eval(i) * tags[index.eval(i)]
+    sigma %= p
+    return mu, sigma
+
+
+def verify(p, sectors, f_key, alpha_key, nchunks, chal_key, chunks, v_max, mu, sigma):
+    """PySwizzle.verify's check (PySwizzle.py:372-395)."""
+    index = KeyedPRF(chal_key, nchunks)
+    v = KeyedPRF(chal_key, v_max)
+    f = KeyedPRF(f_key, p)
+    alpha = KeyedPRF(alpha_key, p)
+    rhs = 0
+    for i in range(0, chunks):
+        rhs += v.eval(i) * f.eval(index.eval(i))
+    for j in range(0, sectors):
+        rhs += alpha.eval(j) * mu[j]
+    return sigma == rhs % p

@@ -54,3 +54,16 @@ def test_c4_strong_scaling_plan():
     assert d["config"]["file_bytes"] == 256 << 30
     d1 = _run("--config", "c4", "--steps", "1")
     assert d1["config"]["pieces_rank0"] == 2      # 256 GiB does not fit one GPU's HBM with its tags
+
+
+def test_multi_gpu_default_is_configs3():
+    """`bench.py --gpus N` with N > 1 and no --config measures configs[3] (one
+    256 GiB file sharded over the N ranks, strong scaling), the N = 1 default
+    stays configs[2] (the driver's 8-GPU run must measure the
+    BASELINE config)."""
+    d = _run("--gpus", "2", "--steps", "1")
+    assert d["scaling"] == "strong" and d["config"]["file_bytes"] == 256 << 30
+    assert d["config"]["workload"].startswith("configs[3]")
+    assert d["config"]["blocks_summed"] == d["config"]["blocks_total"] == (256 << 30) // 512 + 1
+    d1 = _run("--steps", "1")
+    assert d1["config"]["workload"].startswith("configs[2]") and d1["scaling"] == "weak"

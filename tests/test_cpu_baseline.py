@@ -31,6 +31,37 @@ def test_golden_encode_cases(cpu, golden_encode):
     assert n == 176
 
 
+def test_golden_prove_cases(cpu, golden_encode):
+    """The native prove (configs[4]'s "cxx Swizzle" CPU row) == the
+    reference's proofs for every golden case and both challenges
+    (PySwizzle.py:333-370), on 1-3 threads."""
+    n = 0
+    for c in golden_encode["cases"]:
+        p = int(c["prime"], 16)
+        data = bytes.fromhex(c["data"])
+        tags = [int(t, 16) for t in c["tags"]]
+        for chn, prn in (("chal", "proof"), ("chal2", "proof2")):
+            ch = c[chn]
+            mu, sg = cpu.prove(p, c["sectors"], bytes.fromhex(ch["key"]), ch["chunks"], int(ch["v_max"], 16),
+                               tags, data, threads=1 + n % 3)
+            assert mu == [int(m, 16) for m in c[prn]["mu"]], c["name"]
+            assert sg == int(c[prn]["sigma"], 16), c["name"]
+            n += 1
+    assert n == 352
+
+
+def test_prove_many_threads_vs_oracle(cpu, oracle):
+    """A 10,000-index challenge over a 3 MiB file on 16 threads (the bench's
+    configs[4] row shape) == the oracle's prove."""
+    p = int("db8709c32591ddc589b5c3c0986f92e0d11205b943c23a7e419e6c35b0256e6b", 16)
+    data = splitmix_bytes(0x5EED0005, 0, (3 << 20) + 99)
+    fk, ak = hashlib.sha256(b"hb-bench-f").digest(), hashlib.sha256(b"hb-bench-alpha").digest()
+    tags = cpu.encode(p, 16, fk, ak, data, threads=8)
+    key = hashlib.sha256(b"hb-bench-challenge").digest()
+    got = cpu.prove(p, 16, key, 10000, p, tags, data, threads=16)
+    assert got == oracle.prove(p, 16, key, 10000, p, tags, data)
+
+
 def test_golden_file_cases(cpu, golden_files):
     for c in golden_files["cases"]:
         p = int(c["prime"], 16)

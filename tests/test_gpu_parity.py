@@ -493,6 +493,57 @@ def test_device_resident_4_5gib_sampled_vs_oracle(nat, oracle):
         tb.free()
 
 
+def test_prove_host_file_multi_batch(nat, oracle, monkeypatch):
+    """The host-file prove's batched path (hb_runtime.cpp prove_impl): the
+    challenged blocks of a host-resident file gathered by several host
+    threads into two pinned buffers, batch k + 1 gathered while batch k is
+    copied and summed, partial sums accumulated across batches.  Batches are
+    shrunk by the HB_TEST_PROVE_BATCH hook to 2,500 blocks so that a 7,777-index
+    challenge runs 4 batches (3 of them gathered on 4 threads); a 255-bit prime
+    (31-byte sectors, 10 per block: C = 310) puts each batch's tag region at an
+    unaligned offset of its staging buffer.  == the oracle and == the same
+    proof with everything device-resident.  Reference: PySwizzle.py:351-368."""
+    from conftest import load_golden
+    p = int(load_golden("primes.json")["p255"], 16)
+    S, ss = 10, 31
+    C, w = S * ss, 32
+    L = 3 * (1 << 20) + 123
+    nb = L // C + 1
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * w)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 77))
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, tb.p)
+        htags = tb.download()
+        hdata = buf.download()
+        hd = ctypes.create_string_buffer(hdata, L)
+        ht = ctypes.create_string_buffer(htags, len(htags))
+        key = hashlib.sha256(b"multi-batch").digest()
+        pb = nat.be(p)
+        chunks = 7777
+        res = []
+        monkeypatch.setenv("HB_GATHER_THREADS", "4")
+        for tptr, dptr, flags, batch in ((tb.p, buf.p, 3, None), (ht, hd, 0, "2500"), (tb.p, hd, 2, "2500"),
+                                         (ht, hd, 0, None)):
+            if batch:
+                monkeypatch.setenv("HB_TEST_PROVE_BATCH", batch)
+            else:
+                monkeypatch.delenv("HB_TEST_PROVE_BATCH", raising=False)
+            mu = ctypes.create_string_buffer(w * S)
+            sg = ctypes.create_string_buffer(w)
+            ctx.check(nat.lib().hb_prove(ctx.h, pb, len(pb), S, key, 32, chunks, pb, len(pb), tptr, nb, dptr, L,
+                                         flags, mu, sg))
+            res.append((mu.raw, sg.raw))
+        assert res[0] == res[1] == res[2] == res[3]
+        omu, osg = oracle.prove(p, S, key, chunks, p, split_tags(htags, w), hdata)
+        assert [int.from_bytes(res[1][0][j * w:(j + 1) * w], "big") for j in range(S)] == omu
+        assert int.from_bytes(res[1][1], "big") == osg
+    finally:
+        buf.free()
+        tb.free()
+
+
 def test_prove_mixed_residency_equals_device(nat, oracle):
     """hb_prove with the file on the device and the tags on the host (the tags
     are uploaded, the file is not copied back), and the other way round, ==

@@ -140,6 +140,27 @@ def test_pure_python_port_matches_golden(golden_encode):
     assert n > 100
 
 
+def test_pure_python_port_prove_verify_match_golden(golden_encode):
+    """pyswizzle_port.prove / verify (the "PySwizzle" prove row) == the
+    reference's proofs and verdicts."""
+    import io
+    from oracle import pyswizzle_port as PP
+    n = 0
+    for c in golden_encode["cases"]:
+        if c["len"] > 2000:
+            continue
+        p = int(c["prime"], 16)
+        tags = [int(t, 16) for t in c["tags"]]
+        f = io.BytesIO(bytes.fromhex(c["data"]))
+        ch, pr = c["chal"], c["proof"]
+        mu, sg = PP.prove(p, c["sectors"], f, bytes.fromhex(ch["key"]), ch["chunks"], int(ch["v_max"], 16), tags)
+        assert mu == [int(m, 16) for m in pr["mu"]] and sg == int(pr["sigma"], 16), c["name"]
+        assert PP.verify(p, c["sectors"], bytes.fromhex(c["f_key"]), bytes.fromhex(c["alpha_key"]), len(tags),
+                         bytes.fromhex(ch["key"]), ch["chunks"], int(ch["v_max"], 16), mu, sg)
+        n += 1
+    assert n > 100
+
+
 def _merkle_file(name):
     import hashlib
     from conftest import fixture_file
