@@ -71,6 +71,7 @@ SIGNATURES = [
     ("hb_stream_read", _c.c_int, [_P, _P, _c.c_uint64, _c.POINTER(_c.c_double)]),
     ("hb_ctx_set_stream", _c.c_int, [_P, _P]),
     ("hb_ctx_wait", _c.c_int, [_P, _c.POINTER(_c.c_uint64)]),
+    ("hb_ctx_prepare", _c.c_int, [_P, _c.c_uint32]),
     ("hb_merkle_offsets", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint64, _c.c_uint64, _c.c_uint64, _P]),
     ("hb_merkle_chunk_hmacs", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint64, _P, _c.c_uint64, _P,
                                          _c.c_uint64, _P]),
@@ -134,6 +135,16 @@ class Context(object):
     def check(self, rc):
         if rc != 0:
             raise HeartbeatError(lib().hb_last_error(self.h).decode("utf-8", "replace"))
+
+    def prepare(self, prime_bits):
+        """Load the GPU code that encodes / proves with a prime of this size
+        launch (hb_ctx_prepare), so that the first such call does not pay it.
+        A no-op for an experiment build from before this entry point."""
+        L = lib()
+        if not hasattr(L, "hb_ctx_prepare"):
+            return
+        with self.lock:
+            self.check(L.hb_ctx_prepare(self.h, int(prime_bits)))
 
     def last_kernel_ms(self):
         ms = ctypes.c_double()

@@ -34,6 +34,14 @@ struct HbRetry {
 // MFMA MAC (hb_mfma_block_acc): the 256-bit sector MAC as an int8 matrix
 // product; sectors per block it accepts (column sums stay inside int32)
 #define HB_MFMA_MAX_S 2048u
+// A-operand tiles per sector: 1 (dense reduced digits: 32 output digits) or
+// 2 (HB_MFMA_TOEPLITZ, the A/B variant: 64 output digits of the unreduced
+// product, half of each tile zero)
+#if defined(HB_MFMA_TOEPLITZ)
+#define HB_MFMA_NT 2
+#else
+#define HB_MFMA_NT 1
+#endif
 
 template <int NL>
 struct EncodeArgs {
@@ -55,9 +63,13 @@ struct EncodeArgs {
     unsigned long long *retry_count;
     u64 retry_cap;
     // MFMA MAC (256-bit primes, 32-byte aligned sectors): A-operand fragments
-    // of the signed base-256 digits of alpha_j R mod p ([2][S][64 lanes][16 B])
-    // and the constant kz = Q sum_j (alpha_j R mod p) mod p + p 2^268
-    // (Q = 0x8080..80: the sectors enter the product as bytes - 128)
+    // ([HB_MFMA_NT][S][64 lanes][16 B]) and the constant kz (hb_runtime.cpp,
+    // mfma_tables): the 32 signed base-256 digits of r_jk = alpha_j R 256^(31-k)
+    // mod p, one per sector byte k (dense), kz = 128 sum_jk r_jk + p 2^40; or,
+    // with HB_MFMA_TOEPLITZ, the 33-digit Toeplitz band of alpha_j R mod p and
+    // kz = Q sum_j (alpha_j R mod p) mod p + p 2^268 (Q = 0x8080..80: the
+    // sectors enter the product as bytes - 128).  mfma: 1 sector loads,
+    // 2 whole-line loads (hb_line_loads)
     u32 mfma;
     const u32 *afrag;
     u32 kz[2 * NL + 1];
@@ -108,6 +120,14 @@ struct ProveArgs {
     unsigned long long *queue;    // 2 slots: index engine, v engine
     unsigned int *flags;          // bit 0: an index >= #tags (cxx prf after 81 tries)
     u64 qchunk;                   // jobs per queue refill
+    // device-resident file and tags (PySwizzle prove): the index half touches
+    // every challenged block's lines and tag as its index is found, while the
+    // v chain still runs, so that stage 2's gathers find them nearer than HBM
+    // (nullptr: off)
+    const unsigned char *pf_data;
+    const unsigned char *pf_tags;
+    u64 pf_len, pf_C;
+    u32 pf_tw;
 };
 
 // Weighted sums  sum_i w_i * value_{col}(i)  mod p  (w_i in Montgomery form);

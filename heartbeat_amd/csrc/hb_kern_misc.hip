@@ -5,9 +5,9 @@
 
 hipError_t hb_launch_prefix(const PrefixArgs &A, int nr, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
-    if (nr == 14) hipLaunchKernelGGL((hb_prefix_kernel<14>), g, b, 0, s, A);
-    else if (nr == 12) hipLaunchKernelGGL((hb_prefix_kernel<12>), g, b, 0, s, A);
-    else hipLaunchKernelGGL((hb_prefix_kernel<10>), g, b, 0, s, A);
+    if (nr == 14) HB_LAUNCH((hb_prefix_kernel<14>), g, b, s, A);
+    else if (nr == 12) HB_LAUNCH((hb_prefix_kernel<12>), g, b, s, A);
+    else HB_LAUNCH((hb_prefix_kernel<10>), g, b, s, A);
     return hipGetLastError();
 }
 

@@ -476,8 +476,11 @@ __device__ __forceinline__ bool hb_block_full(const EncodeArgs<NL> &A, u64 job) 
 
 // Wave-uniform call.  Returns whether THIS lane's T is valid (active lane,
 // block entirely inside the data); T has 2NL+1 = 17 limbs.  Lane half g
-// (lanes 32g .. 32g+31) owns group g's blocks.  After both groups every lane
-// holds, per group, the 64-bit limbs 2k + h (h = its half) of the group's
+// (lanes 32g .. 32g+31) owns group g's blocks.  Per sector ONE MFMA with the
+// dense A tile of the reduced digits (hb_runtime.cpp, mfma_tables) gives the
+// 32 output digits of the group's blocks, i.e. 8 signed 64-bit limbs (with
+// HB_MFMA_TOEPLITZ two MFMAs, 64 digits, 16 limbs).  After both groups every
+// lane holds, per group, the limbs 2k + h (h = its half) of the group's
 // column-n block; one v_permlane32_swap per dword (lanes 32-63 of the first
 // operand <-> lanes 0-31 of the second, with G0 first and G1 second) then
 // leaves every lane with the EVEN limbs of its own block in the first result
@@ -543,10 +546,14 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
     const u32 l = hb_lane_id(), h = l >> 5, n = l & 31u;
     const bool mine = active && hb_block_full(A, job);
     const u32 S = A.S;
-    long long G[2][8];   // G[g][k]: limb 2k + h of group g's column-n block
+    constexpr int NK = 4 * HB_MFMA_NT;   // limbs per lane half and group
+    long long G[2][NK];   // G[g][k]: limb 2k + h of group g's column-n block
 #pragma unroll
     for (u32 g = 0; g < 2; ++g) {
-        hb_i32x16 acc0 = {}, acc1 = {};
+        hb_i32x16 acc0 = {};
+#if defined(HB_MFMA_TOEPLITZ)
+        hb_i32x16 acc1 = {};
+#endif
 #if !defined(HB_NO_LINE_LOADS)
         if (A.mfma == 2) {
             // load r of lane (h, 4q + i) reads block 4q + r of the group (lane 32 g + 4q + r's)
@@ -565,9 +572,10 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const hb_i32x4 bb = V[r] ^ (int32_t)0x80808080;
-                    const hb_i32x4 a0 = afl[(j0 + r) * 64 + l], a1 = afl[(S + j0 + r) * 64 + l];
-                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bb, acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bb, acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(afl[(j0 + r) * 64 + l], bb, acc0, 0, 0, 0);
+#if defined(HB_MFMA_TOEPLITZ)
+                    acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(afl[(S + j0 + r) * 64 + l], bb, acc1, 0, 0, 0);
+#endif
                 }
             }
         } else
@@ -594,9 +602,10 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
                 const bool in = j0 + jj < S;
                 const u32 j = in ? j0 + jj : S - 1;
                 const hb_i32x4 bb = in ? b[jj] ^ (int32_t)0x80808080 : hb_i32x4{0, 0, 0, 0};
-                const hb_i32x4 a0 = afl[j * 64 + l], a1 = afl[(S + j) * 64 + l];
-                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bb, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bb, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(afl[j * 64 + l], bb, acc0, 0, 0, 0);
+#if defined(HB_MFMA_TOEPLITZ)
+                acc1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(afl[(S + j) * 64 + l], bb, acc1, 0, 0, 0);
+#endif
             }
         }
         }
@@ -606,13 +615,15 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
         for (int q = 0; q < 4; ++q) {
             G[g][q] = (long long)acc0[4 * q] + ((long long)acc0[4 * q + 1] << 8) +
                       ((long long)acc0[4 * q + 2] << 16) + ((long long)acc0[4 * q + 3] << 24);
+#if defined(HB_MFMA_TOEPLITZ)
             G[g][4 + q] = (long long)acc1[4 * q] + ((long long)acc1[4 * q + 1] << 8) +
                           ((long long)acc1[4 * q + 2] << 16) + ((long long)acc1[4 * q + 3] << 24);
+#endif
         }
     }
-    long long ev[8], od[8];   // limbs 2k and 2k + 1 of this lane's own block
+    long long ev[NK], od[NK];   // limbs 2k and 2k + 1 of this lane's own block
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < NK; ++k) {
         const auto lo = __builtin_amdgcn_permlane32_swap((int)(u32)G[0][k], (int)(u32)G[1][k], false, false);
         const auto hi = __builtin_amdgcn_permlane32_swap((int)(G[0][k] >> 32), (int)(G[1][k] >> 32), false, false);
         ev[k] = (long long)(((u64)(u32)hi[0] << 32) | (u32)lo[0]);
@@ -623,7 +634,7 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
 #pragma unroll
     for (int t = 0; t <= 2 * NL; ++t) {
         long long x = (long long)A.kz[t] + carry;
-        if (t < 2 * NL) x += (t & 1) ? od[t >> 1] : ev[t >> 1];
+        if (t < 2 * NK) x += (t & 1) ? od[t >> 1] : ev[t >> 1];
         T[t] = (u32)x;
         carry = x >> 32;
     }
@@ -725,15 +736,15 @@ template <int NL, int NR, int ALIGN>
 __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
     // MFMA MAC for 256-bit primes with aligned full-width sectors (A.mfma set by the host)
     constexpr bool MF = NL == 8 && ALIGN == 16;
-    // MF: the T-table image plus the MFMA A fragments (2 x S x 1 KiB, S <= 16):
-    // 160 KiB, still one workgroup per CU
-    constexpr u32 AFW = MF ? 2u * HB_MFMA_LDS_S * 64u * 4u : 0u;
+    // MF: the T-table image plus the MFMA A fragments (HB_MFMA_NT x S x 1 KiB,
+    // S <= 16): 144 KiB (160 with HB_MFMA_TOEPLITZ), one workgroup per CU
+    constexpr u32 AFW = MF ? HB_MFMA_NT * HB_MFMA_LDS_S * 64u * 4u : 0u;
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS + AFW];
     const bool alds = MF && A.mfma && A.S <= HB_MFMA_LDS_S;
     if (alds) {
         const uint4 *src = reinterpret_cast<const uint4 *>(A.afrag);
         uint4 *dst = reinterpret_cast<uint4 *>(lds + HB_LDS_WORDS);
-        for (u32 k = threadIdx.x; k < 2u * A.S * 64u; k += blockDim.x) dst[k] = src[k];
+        for (u32 k = threadIdx.x; k < HB_MFMA_NT * A.S * 64u; k += blockDim.x) dst[k] = src[k];
     }
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
@@ -879,6 +890,14 @@ struct ProveIdxHandler {
         // on which the reference's t.sigma().at(index) throws: flagged here,
         // raised by the host; stage 2 reads such a term as 0
         if (ix >= A.ntags) atomicOr(A.flags, 1u);
+        if (A.pf_data && ix < A.ntags) {
+            // one byte of each 128-byte line of the block, and its tag; the
+            // impossible store (job < n) keeps the loads
+            const u64 b0 = ix * A.pf_C, b1 = b0 + A.pf_C < A.pf_len ? b0 + A.pf_C : A.pf_len;
+            u32 x = A.pf_tags[ix * A.pf_tw];
+            for (u64 o = b0; o < b1; o += 128) x ^= A.pf_data[o];
+            if (x == 0x9e3779b9u && job == ~0ull) atomicOr(A.flags, 1u << 31);
+        }
     }
 };
 
@@ -1074,13 +1093,25 @@ __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
 
 // ------------------------------------------------------------------ launchers
 // Plain C++ entry points for hb_runtime.cpp (explicit instantiation per
-// limb count NL, AES rounds NR and sector alignment class).
+// limb count NL, AES rounds NR and sector alignment class).  A grid of 0
+// launches nothing: it only makes the runtime load the kernel's code object
+// (hb_ctx_prepare), which otherwise happens inside the first launch.
+template <class K>
+__host__ inline void hb_load_kernel(K *k) {
+    hipFuncAttributes fa;
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(k));
+}
+#define HB_LAUNCH(KT, G, B, S, A)                          \
+    do {                                                   \
+        if ((G).x) hipLaunchKernelGGL(KT, G, B, 0, S, A);  \
+        else hb_load_kernel(&KT);                          \
+    } while (0)
 // pass: 0 = single-pass engine, 1 = first tries (prefix image), 2 = retry list,
 // 3 = cxx prf encode
 template <int NL, int PASS>
 hipError_t hb_launch_encode_pass(const EncodeArgs<NL> &A, int nr, int align, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
-#define HB_ENC(K, NRV, AL) hipLaunchKernelGGL((K<NL, NRV, AL>), g, b, 0, s, A)
+#define HB_ENC(K, NRV, AL) HB_LAUNCH((K<NL, NRV, AL>), g, b, s, A)
 #define HB_ENC_NR(K, AL) \
     do { if (nr == 14) HB_ENC(K, 14, AL); else if (nr == 12) HB_ENC(K, 12, AL); else HB_ENC(K, 10, AL); } while (0)
 #define HB_ENC_AL(K) do { if (align == 16) HB_ENC_NR(K, 16); else HB_ENC_NR(K, 1); } while (0)
@@ -1112,9 +1143,9 @@ hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int mode, int grid, hipSt
     dim3 g(grid), b(HB_ENGINE_WG);
 #define HB_PRF_NR(M, Q)                                                               \
     do {                                                                              \
-        if (nr == 14) hipLaunchKernelGGL((hb_prf_kernel<NL, 14, M, Q>), g, b, 0, s, A); \
-        else if (nr == 12) hipLaunchKernelGGL((hb_prf_kernel<NL, 12, M, Q>), g, b, 0, s, A); \
-        else hipLaunchKernelGGL((hb_prf_kernel<NL, 10, M, Q>), g, b, 0, s, A);       \
+        if (nr == 14) HB_LAUNCH((hb_prf_kernel<NL, 14, M, Q>), g, b, s, A);          \
+        else if (nr == 12) HB_LAUNCH((hb_prf_kernel<NL, 12, M, Q>), g, b, s, A);     \
+        else HB_LAUNCH((hb_prf_kernel<NL, 10, M, Q>), g, b, s, A);                   \
     } while (0)
     if (mode == 1) {
         if constexpr (NL >= 4) HB_PRF_NR(1, false);   // cxx limits are >= 16 bytes
@@ -1133,15 +1164,15 @@ hipError_t hb_launch_prf(const PrfArgs<NL> &A, int nr, int mode, int grid, hipSt
 template <int NL>
 hipError_t hb_launch_mont(const MontArgs<NL> &A, hipStream_t s) {
     const u64 grid = (A.n + 255) / 256;
-    hipLaunchKernelGGL((hb_mont_kernel<NL>), dim3((u32)grid), dim3(256), 0, s, A);
+    HB_LAUNCH((hb_mont_kernel<NL>), dim3((u32)grid), dim3(256), s, A);
     return hipGetLastError();
 }
 
 template <int NL>
 hipError_t hb_launch_wsum(const WsumArgs<NL> &A, int align, int gridx, hipStream_t s) {
     dim3 g(gridx, A.ncols), b(HB_WSUM_WG);
-    if (align == 16) hipLaunchKernelGGL((hb_wsum_kernel<NL, 16>), g, b, 0, s, A);
-    else hipLaunchKernelGGL((hb_wsum_kernel<NL, 1>), g, b, 0, s, A);
+    if (align == 16) HB_LAUNCH((hb_wsum_kernel<NL, 16>), g, b, s, A);
+    else HB_LAUNCH((hb_wsum_kernel<NL, 1>), g, b, s, A);
     return hipGetLastError();
 }
 
@@ -1153,9 +1184,9 @@ hipError_t hb_launch_prove_prf(const ProveArgs<NL> &A, int nr, int mode_i, int m
     dim3 g(grid), b(HB_ENGINE_WG);
 #define HB_PP(MI, MV, Q)                                                                          \
     do {                                                                                          \
-        if (nr == 14) hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 14, MI, MV, Q>), g, b, 0, s, A); \
-        else if (nr == 12) hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 12, MI, MV, Q>), g, b, 0, s, A); \
-        else hipLaunchKernelGGL((hb_prove_prf_kernel<NL, 10, MI, MV, Q>), g, b, 0, s, A);         \
+        if (nr == 14) HB_LAUNCH((hb_prove_prf_kernel<NL, 14, MI, MV, Q>), g, b, s, A);           \
+        else if (nr == 12) HB_LAUNCH((hb_prove_prf_kernel<NL, 12, MI, MV, Q>), g, b, s, A);      \
+        else HB_LAUNCH((hb_prove_prf_kernel<NL, 10, MI, MV, Q>), g, b, s, A);                    \
     } while (0)
     if (mode_i == 3 && mode_v == 3) HB_PP(0, 0, true);
     else if (mode_i == 0 && mode_v == 0) HB_PP(0, 0, false);

@@ -95,6 +95,7 @@ struct hb_ctx {
     DevBuf ctl;          // wsum column counters + flags (zero between operations)
     DevBuf mseeds, moffs, mdig;   // Merkle chunk seeds, offsets, HMAC digests
     HostBuf gstage[2];   // host-file prove: pinned gather buffers (blocks | tags), double-buffered
+    HostBuf hscratch;    // pinned staging of the encode's small host round trips (alpha, MFMA tables)
     bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
     u32 *hres = nullptr; // pinned host copy of wsum results (+ status)
     size_t hres_n = 0;
@@ -283,6 +284,33 @@ bool full16(const PrimeInfo &pi, int nl, u64 C, const void *base) {
     return pi.ss == 4u * (u32)nl && pi.ss % 16 == 0 && C % 16 == 0 && ((uintptr_t)base % 16) == 0;
 }
 
+// ------------------------------------------------------------------ prepare
+// The HIP runtime loads a translation unit's code object (hb_kern_*.hip, up
+// to ~3 MiB each) at the first launch of one of its kernels.  hb_ctx_prepare
+// does that ahead of the first encode / prove with a prime of the given size:
+// every launcher is called with a grid of 0, which only loads the kernel
+// (hb_kernels.hpp, HB_LAUNCH).
+template <int NL>
+void prepare_nl(hb_ctx *c) {
+    EncodeArgs<NL> E;
+    memset(&E, 0, sizeof E);
+    for (int pass = 0; pass <= 3; ++pass)
+        for (int align : {16, 1}) (void)hb_launch_encode<NL>(E, 14, align, pass, 0, c->stream);
+    PrfArgs<NL> P;
+    memset(&P, 0, sizeof P);
+    for (int mode : {0, 3}) (void)hb_launch_prf<NL>(P, 14, mode, 0, c->stream);
+    MontArgs<NL> M;
+    memset(&M, 0, sizeof M);
+    (void)hb_launch_mont<NL>(M, c->stream);   // n = 0: grid 0
+    WsumArgs<NL> W;
+    memset(&W, 0, sizeof W);
+    for (int align : {16, 1}) (void)hb_launch_wsum<NL>(W, align, 0, c->stream);
+    ProveArgs<NL> V;
+    memset(&V, 0, sizeof V);
+    (void)hb_launch_prove_prf<NL>(V, 14, 3, 3, 0, c->stream);
+    (void)hb_launch_prove_prf<NL>(V, 14, 0, 0, 0, c->stream);
+}
+
 // ------------------------------------------------------------------ encode
 // Retry-list capacity for a launch of nb blocks: the first pass rejects each
 // block with probability q = 1 - p / 2^bitlen(p); room for the mean plus 8
@@ -306,18 +334,141 @@ u64 retry_capacity(const uint8_t *p_be, size_t p_len, u64 nb) {
 }
 
 // Host-built inputs of the MFMA MAC (hb_kernels.hpp, hb_mfma_block_acc) from
-// alpha_j R mod p (c->alpha_mont, on the device): the A-operand fragments of
-// the signed base-256 digit Toeplitz matrices and kz.
+// alpha_j R mod p (c->alpha_mont, on the device): the A-operand fragments and kz.
+//
+// Dense (default): sector j = sum_k u_k 256^(31-k) (big-endian bytes u_k), so
+//     alpha_j R u_j = sum_k u_k r_jk (mod p),  r_jk = alpha_j R 256^(31-k) mod p.
+// Each r_jk is taken as the representative in [-0x8080..80, 0x7f7f..7f] (the
+// range of 32 signed base-256 digits, width 2^256 - 1 >= p) and split into its
+// digits D_jk[c], c < 32; the MFMA then computes, per block, the 32 column
+// sums sum_jk D_jk[c] (u_jk - 128) (|.| <= S 2^19 < 2^31), and
+//     T = sum_c col_c 256^c + kz,  kz = 128 sum_jk r_jk + p 2^40 > 0
+// is = R sum_j alpha_j u_j (mod p) and < 2^297, so the finish's REDC of
+// T + F R gives the tag.  One 32 x 32 tile per sector, every entry used.
+// HB_MFMA_TOEPLITZ (A/B variant): the 33 balanced digits d_i of alpha_j R mod p
+// as the Toeplitz band of the unreduced product (64 output digits, two tiles
+// per sector, half of each zero), kz = Q sum_j alpha_j R mod p + p 2^268.
 // Layouts: 1 = sector loads (slot j holds sector j: lane (h, m) byte e is
 // byte 16 h + e of sector j); 2 = whole-line loads (S % 4 == 0; slot j0 + r,
 // j0 % 4 == 0, holds chunk 4h + r of the line of sectors j0 .. j0+3: byte
 // 16 (r % 2) + e of sector j0 + 2h + r / 2), see hb_line_loads.
 int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
     const int NL = 8;
-    std::vector<u32> am((size_t)S * NL);
-    HB_CHECK(hipMemcpyAsync(am.data(), c->alpha_mont.p, am.size() * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
+    HB_CHECK(c->hscratch.ensure((size_t)S * NL * 4 + (size_t)HB_MFMA_NT * S * 64 * 16), "hipHostMalloc(scratch)");
+    u32 *am = (u32 *)c->hscratch.p;
+    int8_t *frag = (int8_t *)c->hscratch.p + (size_t)S * NL * 4;
+    const size_t frag_bytes = (size_t)HB_MFMA_NT * S * 64 * 16;
+    HB_CHECK(hipMemcpyAsync(am, c->alpha_mont.p, (size_t)S * NL * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
     HB_CHECK(hipStreamSynchronize(c->stream), "alpha PRF");
-    std::vector<int8_t> frag((size_t)2 * S * 64 * 16);
+    // slot s, lane half h, byte e -> (sector j, byte k of sector j)
+    auto src_of = [&](u32 slot, int h, int e, u32 &j, int &k) {
+        if (layout == 2) {
+            const u32 r = slot & 3u;
+            j = (slot & ~3u) + 2u * (u32)h + r / 2u;
+            k = 16 * (int)(r & 1u) + e;
+        } else {
+            j = slot;
+            k = 16 * h + e;
+        }
+    };
+#if !defined(HB_MFMA_TOEPLITZ)
+    // D[(j * 32 + k) * 32 + c]: digit c of r_jk
+    std::vector<int8_t> D((size_t)S * 32 * 32);
+    u64 acc[12] = {0};   // sum_jk (r_jk mod p), then kz
+    u64 nneg = 0;        // representatives r_jk - p taken
+    for (u32 j = 0; j < S; ++j) {
+        u32 x[NL];
+        for (int t = 0; t < NL; ++t) x[t] = am[(size_t)j * NL + t];
+        for (int k = 31; k >= 0; --k) {
+            if (k < 31) {
+                // x = 256 x mod p: eight doublings, each reduced (x < p < 2^256)
+                for (int b = 0; b < 8; ++b) {
+                    u32 top = x[NL - 1] >> 31;
+                    for (int t = NL - 1; t > 0; --t) x[t] = (x[t] << 1) | (x[t - 1] >> 31);
+                    x[0] <<= 1;
+                    bool ge = top != 0;
+                    if (!ge) {
+                        ge = true;
+                        for (int t = NL - 1; t >= 0; --t)
+                            if (x[t] != p[t]) {
+                                ge = x[t] > p[t];
+                                break;
+                            }
+                    }
+                    if (ge) {
+                        u64 br = 0;
+                        for (int t = 0; t < NL; ++t) {
+                            const u64 d = (u64)x[t] - p[t] - br;
+                            x[t] = (u32)d;
+                            br = (d >> 63) & 1u;
+                        }
+                    }
+                }
+            }
+            u64 cy = 0;
+            for (int t = 0; t < NL; ++t) {
+                cy += acc[t] + x[t];
+                acc[t] = (u32)cy;
+                cy >>= 32;
+            }
+            for (int t = NL; t < 12 && cy; ++t) {
+                cy += acc[t];
+                acc[t] = (u32)cy;
+                cy >>= 32;
+            }
+            // representative: r = x if x <= 0x7f..7f, else x - p (two's complement)
+            bool big = false;
+            for (int t = NL - 1; t >= 0; --t)
+                if (x[t] != 0x7f7f7f7fu) {
+                    big = x[t] > 0x7f7f7f7fu;
+                    break;
+                }
+            u32 r[NL];
+            u64 br = 0;
+            for (int t = 0; t < NL; ++t) {
+                const u64 d = (u64)x[t] - (big ? p[t] : 0u) - br;
+                r[t] = (u32)d;
+                br = (d >> 63) & 1u;
+            }
+            nneg += big ? 1u : 0u;
+            int carry = 0;
+            int8_t *d = &D[((size_t)j * 32 + (size_t)k) * 32];
+            for (int i = 0; i < 32; ++i) {
+                const int v = (int)((r[i / 4] >> (8 * (i % 4))) & 0xffu) + carry;
+                carry = v >= 128 ? 1 : 0;
+                d[i] = (int8_t)(v - 256 * carry);
+            }
+            // exact: the digits' carry out cancels the sign (0 for r >= 0, 1 for r < 0)
+            if (carry != (big ? 1 : 0)) return fail(c, HB_EINVAL, "internal: MFMA digit range");
+        }
+    }
+    // kz = 128 sum (r_jk mod p) + p (2^40 - 128 nneg)   (nneg <= 32 S <= 2^16)
+    u64 sh = 0;
+    for (int t = 0; t < 12; ++t) {   // acc *= 128
+        const u64 v = (acc[t] << 7) | sh;
+        sh = acc[t] >> 25;
+        acc[t] = v & 0xffffffffull;
+    }
+    const u64 mult = (1ull << 40) - 128ull * nneg;
+    const u64 mlo = mult & 0xffffffffull, mhi = mult >> 32;
+    u64 cy = 0;
+    for (int t = 0; t < 12; ++t) {
+        const u64 plo = t < NL ? (u64)p[t] * mlo : 0u;                      // < 2^64
+        const u64 phi = t >= 1 && t - 1 < NL ? (u64)p[t - 1] * mhi : 0u;   // < 2^40
+        const unsigned __int128 s = (unsigned __int128)acc[t] + (plo & 0xffffffffull) + phi + cy;
+        acc[t] = (u64)s & 0xffffffffull;
+        cy = (u64)(s >> 32) + (plo >> 32);
+    }
+    for (int t = 0; t <= 2 * NL; ++t) kz[t] = t < 12 ? (u32)acc[t] : 0u;
+    for (u32 slot = 0; slot < S; ++slot)
+        for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 16; ++e) {
+                u32 j;
+                int k;
+                src_of(slot, l >> 5, e, j, k);
+                frag[((size_t)slot * 64 + l) * 16 + e] = D[((size_t)j * 32 + (size_t)k) * 32 + (l & 31)];
+            }
+#else
     std::vector<int> digits((size_t)S * 33);
     Limbs sum(NL, 0);
     for (u32 j = 0; j < S; ++j) {
@@ -338,17 +489,9 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
         for (int t = 0; t < 2; ++t)
             for (int l = 0; l < 64; ++l)
                 for (int e = 0; e < 16; ++e) {
-                    const int h = l >> 5;
                     u32 j;
                     int k;   // byte of sector j (weight 256^(31 - k))
-                    if (layout == 2) {
-                        const u32 r = slot & 3u;
-                        j = (slot & ~3u) + 2u * (u32)h + r / 2u;
-                        k = 16 * (int)(r & 1u) + e;
-                    } else {
-                        j = slot;
-                        k = 16 * h + e;
-                    }
+                    src_of(slot, l >> 5, e, j, k);
                     const int col = 32 * t + (l & 31), i = col - 31 + k;
                     const int *d = &digits[(size_t)j * 33];
                     frag[(((size_t)t * S + slot) * 64 + l) * 16 + e] = (int8_t)(i >= 0 && i <= 32 ? d[i] : 0);
@@ -369,8 +512,9 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
         kz[t] = (u32)carry;
         carry >>= 32;
     }
-    HB_CHECK(c->afrag.ensure(frag.size()), "hipMalloc(afrag)");
-    HB_CHECK(hipMemcpyAsync(c->afrag.p, frag.data(), frag.size(), hipMemcpyHostToDevice, c->stream), "H2D(afrag)");
+#endif
+    HB_CHECK(c->afrag.ensure(frag_bytes), "hipMalloc(afrag)");
+    HB_CHECK(hipMemcpyAsync(c->afrag.p, frag, frag_bytes, hipMemcpyHostToDevice, c->stream), "H2D(afrag)");
     HB_CHECK(hipStreamSynchronize(c->stream), "H2D(afrag)");
     return 0;
 }
@@ -423,11 +567,13 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // alpha_j R mod p, j < S  (alpha = KeyedPRF(alpha_key, p), PySwizzle.py:291,302)
     HB_CHECK(c->alpha_raw.ensure((size_t)S * NL * 4), "hipMalloc");
     HB_CHECK(c->alpha_mont.ensure((size_t)S * NL * 4), "hipMalloc");
+    mark("alpha buffers");
     const bool cxx = flags & HB_PRF_CXX;
     if (cxx && (pi.tw % 16 != 0 || pi.tw > 4u * NL))
         return fail(c, HB_EUNSUPPORTED, "cxx prf mode needs ByteCount(p) to be a multiple of 16");
     int rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, cxx ? 1 : 0);
     if (rc) return rc;
+    mark("alpha PRF");
     rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S);
     if (rc) return rc;
     mark("alpha PRF + Montgomery");
@@ -815,6 +961,13 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         tags = (const uint8_t *)c->tags.p;
         tags_dev = true;
     }
+    if (data_dev && tags_dev && !cxx && !check_all && !getenv("HB_NO_PROVE_PREFETCH")) {
+        PA.pf_data = data;
+        PA.pf_tags = tags;
+        PA.pf_len = len;
+        PA.pf_C = C;
+        PA.pf_tw = pi.tw;
+    }
     // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
     const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
     HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, quad ? 3 : mode_i, quad ? 3 : mode_v, pgrid, c->stream),
@@ -1069,6 +1222,9 @@ int hb_ctx_create(int device, hb_ctx **out) {
         return bad(e, "hipMemcpy");
     if ((e = hipMalloc(&c->queue, 16 * HB_QSLOT * sizeof(unsigned long long))) != hipSuccess) return bad(e, "hipMalloc");
     if ((e = hipMemset(c->queue, 0, 16 * HB_QSLOT * sizeof(unsigned long long))) != hipSuccess) return bad(e, "hipMemset");
+    // pinned staging for the encode's alpha / MFMA-table round trips (S <= 64
+    // without regrowing), allocated here rather than inside the first encode
+    if ((e = c->hscratch.ensure(64u << 10)) != hipSuccess) return bad(e, "hipHostMalloc");
     *out = c;
     return HB_OK;
 }
@@ -1086,6 +1242,7 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->hres) (void)hipHostFree(c->hres);
     c->gstage[0].release();
     c->gstage[1].release();
+    c->hscratch.release();
     if (c->t0) (void)hipFree(c->t0);
     if (c->queue) (void)hipFree(c->queue);
     if (c->k0) (void)hipEventDestroy(c->k0);
@@ -1107,6 +1264,31 @@ int hb_ctx_set_stream(hb_ctx *c, void *stream) {
     // anything enqueued on the new one
     HB_CHECK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    return 0;
+}
+
+int hb_ctx_prepare(hb_ctx *c, uint32_t prime_bits) {
+    if (!c) return HB_EINVAL;
+    HB_CHECK(hipSetDevice(c->device), "hipSetDevice");
+    int nl = nl_for_bits((int)prime_bits);
+    if (!nl) return fail(c, HB_EUNSUPPORTED, "primes above 2048 bits are not supported by this build");
+    if (nl < 8) nl = 8;
+    PrefixArgs PA;
+    memset(&PA, 0, sizeof PA);
+    (void)hb_launch_prefix(PA, 14, 0, c->stream);
+    PrfArgs<2> P2;
+    memset(&P2, 0, sizeof P2);
+    (void)hb_launch_prf<2>(P2, 14, 0, 0, c->stream);
+    switch (nl) {
+    case 8: prepare_nl<8>(c); break;
+    case 16: prepare_nl<16>(c); break;
+    case 32: prepare_nl<32>(c); break;
+#if !defined(HB_NO_NL64)
+    case 64: prepare_nl<64>(c); break;
+#endif
+    default: return fail(c, HB_EUNSUPPORTED, "primes above 2048 bits are not supported by this build");
+    }
+    (void)hipGetLastError();
     return 0;
 }
 

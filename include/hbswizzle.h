@@ -106,6 +106,13 @@ int hb_ctx_set_stream(hb_ctx *ctx, void *stream);
  * this call. */
 int hb_ctx_wait(hb_ctx *ctx, uint64_t *tries_out);
 
+/* Load the GPU code of the kernels that encodes and proves with a prime of
+ * `prime_bits` bits launch, ahead of the first such call (the HIP runtime
+ * otherwise loads a kernel translation unit's code object inside its first
+ * launch: ~5 ms for the 256-bit unit).  Optional; replaces nothing in the
+ * reference (setup, like creating a library handle). */
+int hb_ctx_prepare(hb_ctx *ctx, uint32_t prime_bits);
+
 /* ceil(bitlen(p)/8): width of every tag / mu / sigma value. */
 size_t hb_width(const uint8_t *p_be, size_t p_len);
 

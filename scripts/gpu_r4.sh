@@ -53,6 +53,11 @@ if [ -n "$STATS" ]; then
     step stats_${VNAME} 400 rocprofv3 --kernel-trace --stats -d $OUT/stats_${VNAME} -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity-sample ${BENCHARGS} || exit 1
   done
 fi
+if [ -n "$COLD" ]; then
+  apply base
+  HB_TRACE_PHASES=1 step c4_cold_trace 300 python3 -u bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline --no-parity-sample || exit 1
+  HB_TRACE_PHASES=1 step c3_cold_trace 300 python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-parity-sample || exit 1
+fi
 if [ -n "$FULLBENCH" ]; then
   apply base
   step bench_full 600 python -u bench.py ${FULLBENCH_ARGS} || exit 1

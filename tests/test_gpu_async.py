@@ -107,3 +107,28 @@ def test_async_status_and_timing_accumulate(nat):
     finally:
         buf.free()
         tb.free()
+
+
+def test_prepare_then_encode_on_a_fresh_context(nat, oracle):
+    """hb_ctx_prepare (load the kernels' code objects ahead of the first call)
+    on a fresh context, for every supported prime size; an encode afterwards
+    on it equals the oracle; > 2048 bits is refused like hb_encode refuses it."""
+    from heartbeat_amd.exc import HeartbeatError
+    ctx = nat.Context(0)
+    try:
+        for bits in (8, 255, 256, 512, 1024, 2048):
+            ctx.prepare(bits)
+        with pytest.raises(HeartbeatError):
+            ctx.prepare(2049)
+        p, S, L = P256, 16, 1 << 20
+        nb = L // 512 + 1
+        pb = nat.be(p)
+        data = b"".join(hashlib.sha256(b"prep%d" % i).digest() for i in range(L // 32))
+        tags = ctypes.create_string_buffer(nb * 32)
+        tries = ctypes.c_uint64()
+        ctx.check(nat.lib().hb_encode(ctx.h, pb, len(pb), S, b"f" * 32, b"a" * 32, 32, 0, data, L, nb, tags, 0,
+                                      ctypes.byref(tries)))
+        want = oracle.encode(p, S, b"f" * 32, b"a" * 32, data)
+        assert tags.raw == b"".join(t.to_bytes(32, "big") for t in want)
+    finally:
+        ctx.close()
