@@ -120,14 +120,6 @@ struct ProveArgs {
     unsigned long long *queue;    // 2 slots: index engine, v engine
     unsigned int *flags;          // bit 0: an index >= #tags (cxx prf after 81 tries)
     u64 qchunk;                   // jobs per queue refill
-    // device-resident file and tags (PySwizzle prove): the index half touches
-    // every challenged block's lines and tag as its index is found, while the
-    // v chain still runs, so that stage 2's gathers find them nearer than HBM
-    // (nullptr: off)
-    const unsigned char *pf_data;
-    const unsigned char *pf_tags;
-    u64 pf_len, pf_C;
-    u32 pf_tw;
 };
 
 // Weighted sums  sum_i w_i * value_{col}(i)  mod p  (w_i in Montgomery form);

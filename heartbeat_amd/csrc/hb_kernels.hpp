@@ -890,14 +890,6 @@ struct ProveIdxHandler {
         // on which the reference's t.sigma().at(index) throws: flagged here,
         // raised by the host; stage 2 reads such a term as 0
         if (ix >= A.ntags) atomicOr(A.flags, 1u);
-        if (A.pf_data && ix < A.ntags) {
-            // one byte of each 128-byte line of the block, and its tag; the
-            // impossible store (job < n) keeps the loads
-            const u64 b0 = ix * A.pf_C, b1 = b0 + A.pf_C < A.pf_len ? b0 + A.pf_C : A.pf_len;
-            u32 x = A.pf_tags[ix * A.pf_tw];
-            for (u64 o = b0; o < b1; o += 128) x ^= A.pf_data[o];
-            if (x == 0x9e3779b9u && job == ~0ull) atomicOr(A.flags, 1u << 31);
-        }
     }
 };
 

@@ -961,13 +961,6 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         tags = (const uint8_t *)c->tags.p;
         tags_dev = true;
     }
-    if (data_dev && tags_dev && !cxx && !check_all && !getenv("HB_NO_PROVE_PREFETCH")) {
-        PA.pf_data = data;
-        PA.pf_tags = tags;
-        PA.pf_len = len;
-        PA.pf_C = C;
-        PA.pf_tw = pi.tw;
-    }
     // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
     const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
     HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, quad ? 3 : mode_i, quad ? 3 : mode_v, pgrid, c->stream),

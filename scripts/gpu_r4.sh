@@ -13,13 +13,15 @@ OUT=gpurun_out/${TAG:-r4}
 mkdir -p $OUT
 step() { local name=$1 limit=$2; shift 2; echo "== $name"; timeout -k 10 $limit "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "   rc=$rc"; tail -1 $OUT/$name.log | cut -c1-400; return $rc; }
 # apply a variant spec: exports its assignments in the current shell
+APPLIED=""
 apply() {
   local spec=$1 kv
-  unset HB_LIB_PATH HB_MFMA_SECTOR_LOADS HB_NO_MFMA
+  for kv in $APPLIED; do unset "$kv"; done
+  APPLIED=""
   VNAME=${spec%%:*}
   if [ "$spec" != "$VNAME" ]; then
     IFS=',' read -ra KVS <<< "${spec#*:}"
-    for kv in "${KVS[@]}"; do export "$kv"; done
+    for kv in "${KVS[@]}"; do export "$kv"; APPLIED="$APPLIED ${kv%%=*}"; done
   fi
 }
 if [ -n "$TESTS" ]; then
