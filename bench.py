@@ -191,6 +191,14 @@ class Ranks(object):
 
 
 # ---------------------------------------------------------------- workload
+def workload_name(args, cfg):
+    """The BASELINE config's name, marked when --gib overrides its size (a
+    rehearsal or a test, not that config's measurement)."""
+    if args.gib is None:
+        return cfg["name"]
+    return "%s [--gib %g: %g GiB per rank instead]" % (cfg["name"], args.gib, args.gib)
+
+
 def plan_for(args, cfg, world, rank):
     from heartbeat_amd.shard import shard_plan
     S = cfg["sectors"]
@@ -250,7 +258,7 @@ def dry_run(args, R):
                           **rep, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
                           "scaling": "weak" if cfg["weak"] else "strong", "dry_run": True,
-                          "config": {"workload": cfg["name"], "file_bytes": file_len,
+                          "config": {"workload": workload_name(args, cfg), "file_bytes": file_len,
                                      "blocks_total": plan["total_blocks"], "blocks_summed": int(blocks),
                                      "pieces_rank0": len(pieces)}}), flush=True)
 
@@ -400,7 +408,7 @@ def bench_encode(args, cfg, R):
         "dtype": "u32",
         "data": "synthetic (SplitMix64 random file bytes, seeded keys)",
         "config": {
-            "workload": cfg["name"],
+            "workload": workload_name(args, cfg),
             "file_bytes": file_len,
             "file_bytes_per_rank": length,
             "resident_pieces_per_rank": len(pieces),
@@ -836,7 +844,7 @@ def bench_prove(args, cfg, R):
         "ms_per_step": round(ms, 4), "higher_is_better": False, "scaling": "weak",
         "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (SplitMix64 random file bytes, seeded keys)",
-        "config": {"workload": cfg["name"], "file_bytes": length, "blocks_total": nblocks,
+        "config": {"workload": workload_name(args, cfg), "file_bytes": length, "blocks_total": nblocks,
                    "sectors": S, "prime_bits": 256, "chunks": chunks,
                    "prf": "cxx prf, cxx prove (parity unpinned)" if cxx else "PySwizzle KeyedPRF"},
         "gathered_bytes_per_proof": chunks * (C + w),
