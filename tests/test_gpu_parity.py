@@ -277,6 +277,37 @@ def test_device_resident_64mib_vs_oracle(nat, oracle, S, prime_name):
         tb.free()
 
 
+@pytest.mark.parametrize("prime_name", ["p256", "p256max", "p256lo"])
+@pytest.mark.parametrize("S", [4, 6, 17, 20, 36])
+def test_mfma_mac_sector_counts_vs_oracle(nat, oracle, S, prime_name):
+    """The first pass's MFMA MAC (hb_mfma_block_acc, dense digit tiles from
+    mfma_tables) at the sector counts the 64 MiB test does not reach: S = 4
+    (the smallest MFMA case), 6 and 17 (sector-shaped loads, S % 4 != 0),
+    20 and 36 (whole-line loads), 17 / 20 / 36 with the A fragments read from
+    global memory instead of LDS (S > 16); primes with p just above 2^255
+    (p256lo, half the first tries rejected) and just below 2^256 (p256max: the
+    digit representatives r - p at the edge of their range).  A ragged 2 MiB
+    device-resident file, block_base != 0; every tag == the oracle."""
+    primes = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))
+    p = int(primes[prime_name], 16)
+    L = (2 << 20) + 777
+    C = 32 * S
+    nb = L // C + 1
+    base = 123456789
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * 32)
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 1000 + S))
+        fk, ak = hashlib.sha256(b"mf-f%d" % S).digest(), hashlib.sha256(b"mf-a" + prime_name.encode()).digest()
+        dev_encode(nat, p, S, fk, ak, buf.p, L, nb, tb.p, block_base=base)
+        want = oracle.encode(p, S, fk, ak, buf.download(), block_base=base, nthreads=16)
+        assert split_tags(tb.download(), 32) == want
+    finally:
+        buf.free()
+        tb.free()
+
+
 @pytest.mark.parametrize("S,prime_name", [(16, "p256"), (1, "p256"), (5, "p255"), (16, "p256lo"),
                                           (3, "p1024"), (4, "p61")])
 def test_two_pass_equals_single_pass(nat, S, prime_name):
