@@ -10,7 +10,9 @@
 #define HB_ENGINE_WG 1024
 #endif
 #define HB_ENGINE_WG_PER_CU 1
+#ifndef HB_QUEUE_CHUNK
 #define HB_QUEUE_CHUNK 256
+#endif
 // PRF tries after which a job is abandoned and reported (see hb_engine)
 #define HB_MAX_TRIES 2048u
 // job-queue counters per slot: [0] next job, [1] PRF tries, [2] abandoned jobs,

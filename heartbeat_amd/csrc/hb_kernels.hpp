@@ -492,6 +492,10 @@ __device__ __forceinline__ bool hb_block_full(const EncodeArgs<NL> &A, u64 job) 
 #define HB_MFMA_BATCH 4
 #endif
 #define HB_MFMA_LDS_S 16
+// issue priority of a first try's AES (s_setprio; the rest of the loop runs at 0)
+#ifndef HB_AES_PRIO
+#define HB_AES_PRIO 2
+#endif
 
 // x of lane (l ^ 1) / (l ^ 2) within the lane's quad (DPP quad_perm)
 __device__ __forceinline__ int32_t hb_quad_x1(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, false); }
@@ -773,7 +777,7 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
             // waves in their AES phase go first in issue arbitration, so the
             // LDS stays fed while other waves hash or run the MAC (+0.8 %,
             // same-box A/B, profiles/r02/s13)
-            __builtin_amdgcn_s_setprio(2);
+            __builtin_amdgcn_s_setprio(HB_AES_PRIO);
             ok = hb_prf_first_try<NL, NR>(L, A.prf, A.pfx, A.o0, sr, dig, out);
             __builtin_amdgcn_s_setprio(0);
         }
