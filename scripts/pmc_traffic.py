@@ -28,7 +28,8 @@ def pick(summ, part):
     return {}
 
 
-def main(fetch_csv, write_csv, sq_csv):
+def compute(fetch_csv, write_csv, sq_csv):
+    """The pmc_traffic.json["c3"] record of these three PMC passes."""
     f, w, q = summarize([fetch_csv]), summarize([write_csv]), summarize([sq_csv])
     kb = 1024
     ff, fr, fp = (pick(f, n).get("FETCH_SIZE", 0.0) for n in ("encode_first", "encode_retry", "prefix_kernel"))
@@ -58,6 +59,11 @@ def main(fetch_csv, write_csv, sq_csv):
                       "duration; lds_busy = SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE/8); valu = SQ_INSTS_VALU / "
                       "(256 CUs x GRBM_GUI_ACTIVE/8); SQ_LDS_BANK_CONFLICT = %d" % (sq_csv, sq.get("SQ_LDS_BANK_CONFLICT", -1)),
     }
+    return rec
+
+
+def main(fetch_csv, write_csv, sq_csv):
+    rec = compute(fetch_csv, write_csv, sq_csv)
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     d = json.load(open(path))
     d["c3"] = rec
