@@ -39,6 +39,12 @@ struct HbRetry {
 // A-operand tiles per sector: 1 (dense reduced digits: 32 output digits) or
 // 2 (HB_MFMA_TOEPLITZ, the A/B variant: 64 output digits of the unreduced
 // product, half of each tile zero)
+// The dense MAC's finish: HB_MAC_MONT = Montgomery REDC of T + F R (the
+// tiles carry alpha_j R); HB_MAC_PLAIN = one quotient-estimate reduction of
+// T + F (the tiles carry alpha_j).  Until measured, MONT is the default.
+#if !defined(HB_MAC_PLAIN) && !defined(HB_MAC_MONT)
+#define HB_MAC_MONT
+#endif
 #if defined(HB_MFMA_TOEPLITZ)
 #define HB_MFMA_NT 2
 #else
@@ -66,12 +72,13 @@ struct EncodeArgs {
     u64 retry_cap;
     // MFMA MAC (256-bit primes, 32-byte aligned sectors): A-operand fragments
     // ([HB_MFMA_NT][S][64 lanes][16 B]) and the constant kz (hb_runtime.cpp,
-    // mfma_tables): the 32 signed base-256 digits of r_jk = alpha_j R 256^(31-k)
-    // mod p, one per sector byte k (dense), kz = 128 sum_jk r_jk + p 2^40; or,
+    // mfma_tables): the 32 signed base-256 digits of r_jk = alpha_j 256^(31-k)
+    // mod p, one per sector byte k (dense), kz = 128 sum_jk r_jk + p 2^w; or,
     // with HB_MFMA_TOEPLITZ, the 33-digit Toeplitz band of alpha_j R mod p and
     // kz = Q sum_j (alpha_j R mod p) mod p + p 2^268 (Q = 0x8080..80: the
     // sectors enter the product as bytes - 128).  mfma: 1 sector loads,
-    // 2 whole-line loads (hb_line_loads)
+    // 2 whole-line loads (hb_line_loads), 3 the 16x16x64 MFMA
+    // (hb_mfma16_block_acc)
     u32 mfma;
     const u32 *afrag;
     u32 kz[2 * NL + 1];

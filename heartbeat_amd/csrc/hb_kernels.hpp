@@ -646,6 +646,106 @@ __device__ __forceinline__ bool hb_mfma_block_acc(const EncodeArgs<NL> &A, const
     return mine;
 }
 
+// The MAC on v_mfma_i32_16x16x64_i8 (EncodeArgs::mfma == 3, dense tiles,
+// S % 2 == 0).  Its B operand is exactly the whole-line load shape: lane
+// (q, n) = (l >> 4, l & 15) holds bytes 16 q .. 16 q + 15 of column n's
+// 64-byte K slice, so for sectors 2p, 2p+1 the four lanes n, n+16, n+32, n+48
+// read one contiguous 64-byte half line of block n: every load instruction
+// requests 16 whole 64-byte pieces and no lane exchange is needed before the
+// MFMA (the 32x32x32 line path, hb_line_loads, spends 2 x 16 DPP moves and
+// selects per 4 sectors on that).  Group g (g < 4) is the 16 blocks of lanes
+// 16 g .. 16 g + 15; two 16-row tiles (output digits 0-15, 16-31) per K
+// slice, their A fragments read once per slice for all four groups.
+// Afterwards lane (q, n) holds, per group g, limbs q and 4 + q of block
+// 16 g + n; a 4 x 4 transpose of (group, lane row) -- one v_permlane32_swap
+// stage and one v_permlane16_swap stage per dword -- leaves every lane with
+// the 8 limbs of its own block.
+template <int NL, bool ALDS>
+__device__ __forceinline__ bool hb_mfma16_block_acc(const EncodeArgs<NL> &A, const hb_i32x4 *afl, u64 job,
+                                                    bool active, u32 T[2 * NL + 1]) {
+    static_assert(NL == 8, "MFMA MAC: 256-bit primes only");
+    const u32 l = hb_lane_id(), q = l >> 4, n = l & 15u;
+    const bool mine = active && hb_block_full(A, job);
+    const u32 np = A.S / 2;   // K slices of 64 bytes (2 sectors)
+    const unsigned char *blk[4];
+    bool okg[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int src = (int)(16 * g + n);
+        const u64 jb = (u64)__shfl((long long)job, src);
+        okg[g] = __shfl((int)mine, src) != 0;
+        blk[g] = A.data + jb * A.C + 16u * q;
+    }
+    hb_i32x4 acc[4][2];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g][0] = acc[g][1] = hb_i32x4{0, 0, 0, 0};
+    auto slice = [&](const hb_i32x4 b[4], u32 p) {
+        const hb_i32x4 a0 = afl[(2 * p) * 64 + l], a1 = afl[(2 * p + 1) * 64 + l];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const hb_i32x4 bb = b[g] ^ (int32_t)0x80808080;
+            acc[g][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bb, acc[g][0], 0, 0, 0);
+            acc[g][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bb, acc[g][1], 0, 0, 0);
+        }
+    };
+    u32 p = 0;
+    // two slices (one 128-byte line of every block) per round of loads
+    for (; p + 1 < np; p += 2) {
+        hb_i32x4 b0[4], b1[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            b0[g] = okg[g] ? *reinterpret_cast<const hb_i32x4 *>(blk[g] + 64u * p) : hb_i32x4{0, 0, 0, 0};
+            b1[g] = okg[g] ? *reinterpret_cast<const hb_i32x4 *>(blk[g] + 64u * (p + 1)) : hb_i32x4{0, 0, 0, 0};
+        }
+        slice(b0, p);
+        slice(b1, p + 1);
+    }
+    if (p < np) {
+        hb_i32x4 b0[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+            b0[g] = okg[g] ? *reinterpret_cast<const hb_i32x4 *>(blk[g] + 64u * p) : hb_i32x4{0, 0, 0, 0};
+        slice(b0, p);
+    }
+    // X[g][d]: dwords of limbs q (d = 0, 1) and 4 + q (d = 2, 3) of block 16 g + n
+    u32 X[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const hb_i32x4 &a = acc[g][t];
+            const long long v = (long long)a[0] + ((long long)a[1] << 8) + ((long long)a[2] << 16) +
+                                ((long long)a[3] << 24);
+            X[g][2 * t] = (u32)v;
+            X[g][2 * t + 1] = (u32)((u64)v >> 32);
+        }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const auto s02 = __builtin_amdgcn_permlane32_swap((int)X[0][d], (int)X[2][d], false, false);
+        const auto s13 = __builtin_amdgcn_permlane32_swap((int)X[1][d], (int)X[3][d], false, false);
+        const auto s01 = __builtin_amdgcn_permlane16_swap((int)s02[0], (int)s13[0], false, false);
+        const auto s23 = __builtin_amdgcn_permlane16_swap((int)s02[1], (int)s13[1], false, false);
+        X[0][d] = (u32)s01[0];
+        X[1][d] = (u32)s01[1];
+        X[2][d] = (u32)s23[0];
+        X[3][d] = (u32)s23[1];
+    }
+    // slot s: limbs s and 4 + s of this lane's block.  T = kz + sum_t L_t 2^(32 t)
+    long long carry = 0;
+#pragma unroll
+    for (int t = 0; t <= 2 * NL; ++t) {
+        long long x = (long long)A.kz[t] + carry;
+        if (t < 8) {
+            const int sl = t & 3, hi = t >> 2;
+            x += (long long)(((u64)X[sl][2 * hi + 1] << 32) | X[sl][2 * hi]);
+        }
+        T[t] = (u32)x;
+        carry = x >> 32;
+    }
+    return mine;
+}
+
+#if defined(HB_MAC_MONT)
 // tag = (T + F R) R^-1 mod p  (T from hb_mfma_block_acc; F < 2^256 at limbs NL..)
 template <int NL>
 __device__ __forceinline__ void hb_finish_T(u32 T[2 * NL + 1], const u32 F[NL], const ModP<NL> &M, u32 out[NL]) {
@@ -660,12 +760,31 @@ __device__ __forceinline__ void hb_finish_T(u32 T[2 * NL + 1], const u32 F[NL], 
     hb_redc<NL>(T, M, v);
     hb_reduce_small<NL>(v, M, out);
 }
+#else
+// tag = (T + F) mod p: T (from hb_mfma_block_acc) = sum_j alpha_j m_j mod p
+// plus a multiple of p, < 2^282 (hb_runtime.cpp, mfma_tables), so T + F fits
+// NL + 1 limbs with a quotient below 2^27 -- one quotient-estimate reduction
+// (hb_reduce_small), no Montgomery REDC
+template <int NL>
+__device__ __forceinline__ void hb_finish_T(u32 T[2 * NL + 1], const u32 F[NL], const ModP<NL> &M, u32 out[NL]) {
+    u32 v[NL + 1];
+    u64 c = 0;
+    HB_UNROLL
+    for (int t = 0; t < NL; ++t) {
+        c += (u64)T[t] + F[t];
+        v[t] = (u32)c;
+        c >>= 32;
+    }
+    v[NL] = T[NL] + (u32)c;
+    hb_reduce_small<NL>(v, M, out);
+}
+#endif
 
 // End of the first try of every lane's block (wave-uniform call): accepted
 // blocks are tagged, rejected ones go to the retry list with their shift
 // register (and, with the MFMA MAC, with sum_j alpha_j m_j mod p, so that the
 // retry pass only adds F).  With the MFMA MAC both cases are ONE reduction,
-// (T + F' R) R^-1 mod p with F' = F (accepted) or 0 (rejected): with ~14 %
+// (T + F') mod p with F' = F (accepted) or 0 (rejected) (hb_finish_T): with ~14 %
 // rejected first tries nearly every wave has lanes of both kinds, and two
 // divergent reductions would cost both per wave.
 template <int NL, int NR, int ALIGN, class H>
@@ -768,8 +887,18 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
         if (0)
 #endif
         if constexpr (MF) {
-            if (alds) tmine = hb_mfma_block_acc<NL, true>(A, reinterpret_cast<const hb_i32x4 *>(lds + HB_LDS_WORDS), job, act, T);
-            else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, reinterpret_cast<const hb_i32x4 *>(A.afrag), job, act, T);
+            // two call sites, so that each sees which memory its A fragments
+            // are in (LDS: ds_read_b128; global: global_load_dwordx4)
+            const hb_i32x4 *afl_lds = reinterpret_cast<const hb_i32x4 *>(lds + HB_LDS_WORDS);
+            const hb_i32x4 *afl_glb = reinterpret_cast<const hb_i32x4 *>(A.afrag);
+#if !defined(HB_MFMA_TOEPLITZ)
+            if (A.mfma == 3) {
+                if (alds) tmine = hb_mfma16_block_acc<NL, true>(A, afl_lds, job, act, T);
+                else tmine = hb_mfma16_block_acc<NL, false>(A, afl_glb, job, act, T);
+            } else
+#endif
+            if (alds) tmine = hb_mfma_block_acc<NL, true>(A, afl_lds, job, act, T);
+            else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, afl_glb, job, act, T);
         }
         u32 out[NL], sr[4], ok;
         {

@@ -333,34 +333,47 @@ u64 retry_capacity(const uint8_t *p_be, size_t p_len, u64 nb) {
     return cap >= (double)nb ? nb : (u64)cap;
 }
 
-// Host-built inputs of the MFMA MAC (hb_kernels.hpp, hb_mfma_block_acc) from
-// alpha_j R mod p (c->alpha_mont, on the device): the A-operand fragments and kz.
+// Host-built inputs of the MFMA MAC (hb_kernels.hpp, hb_mfma_block_acc /
+// hb_mfma16_block_acc) from alpha_j (c->alpha_raw, on the device): the
+// A-operand fragments and kz.
 //
 // Dense (default): sector j = sum_k u_k 256^(31-k) (big-endian bytes u_k), so
-//     alpha_j R u_j = sum_k u_k r_jk (mod p),  r_jk = alpha_j R 256^(31-k) mod p.
+//     alpha_j u_j = sum_k u_k r_jk (mod p),  r_jk = alpha_j 256^(31-k) mod p.
 // Each r_jk is taken as the representative in [-0x8080..80, 0x7f7f..7f] (the
 // range of 32 signed base-256 digits, width 2^256 - 1 >= p) and split into its
 // digits D_jk[c], c < 32; the MFMA then computes, per block, the 32 column
 // sums sum_jk D_jk[c] (u_jk - 128) (|.| <= S 2^19 < 2^31), and
-//     T = sum_c col_c 256^c + kz,  kz = 128 sum_jk r_jk + p 2^40 > 0
-// is = R sum_j alpha_j u_j (mod p) and < 2^297, so the finish's REDC of
-// T + F R gives the tag.  One 32 x 32 tile per sector, every entry used.
+//     T = sum_c col_c 256^c + kz,  kz = 128 sum_jk r_jk + p 2^w > 0
+// is = sum_j alpha_j u_j (mod p) and < 2^282 (w below), so the finish is
+// (T + F) mod p by one quotient-estimate reduction.  One tile row per output
+// digit, every entry used.  HB_MAC_MONT (A/B variant): r_jk carries R
+// (alpha_j R mod p, c->alpha_mont), w = 40, T < 2^297 and the finish is the
+// REDC of T + F R.
 // HB_MFMA_TOEPLITZ (A/B variant): the 33 balanced digits d_i of alpha_j R mod p
 // as the Toeplitz band of the unreduced product (64 output digits, two tiles
 // per sector, half of each zero), kz = Q sum_j alpha_j R mod p + p 2^268.
 // Layouts: 1 = sector loads (slot j holds sector j: lane (h, m) byte e is
 // byte 16 h + e of sector j); 2 = whole-line loads (S % 4 == 0; slot j0 + r,
 // j0 % 4 == 0, holds chunk 4h + r of the line of sectors j0 .. j0+3: byte
-// 16 (r % 2) + e of sector j0 + 2h + r / 2), see hb_line_loads.
+// 16 (r % 2) + e of sector j0 + 2h + r / 2), see hb_line_loads; 3 = the
+// 16x16x64 MFMA (S % 2 == 0, dense only), see hb_mfma16_block_acc.
 int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
     const int NL = 8;
     HB_CHECK(c->hscratch.ensure((size_t)S * NL * 4 + (size_t)HB_MFMA_NT * S * 64 * 16), "hipHostMalloc(scratch)");
     u32 *am = (u32 *)c->hscratch.p;
     int8_t *frag = (int8_t *)c->hscratch.p + (size_t)S * NL * 4;
     const size_t frag_bytes = (size_t)HB_MFMA_NT * S * 64 * 16;
-    HB_CHECK(hipMemcpyAsync(am, c->alpha_mont.p, (size_t)S * NL * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
+#if !defined(HB_MFMA_TOEPLITZ) && !defined(HB_MAC_MONT)
+    // the dense tiles carry alpha_j itself (the finish adds F and reduces,
+    // no REDC); HB_MAC_MONT / the Toeplitz MAC: alpha_j R mod p
+    const void *asrc = c->alpha_raw.p;
+#else
+    const void *asrc = c->alpha_mont.p;
+#endif
+    HB_CHECK(hipMemcpyAsync(am, asrc, (size_t)S * NL * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
     HB_CHECK(hipStreamSynchronize(c->stream), "alpha PRF");
-    // slot s, lane half h, byte e -> (sector j, byte k of sector j)
+    // layouts 1, 2 (32x32x32 B operand): slot s, lane half h, byte e ->
+    // (sector j, byte k of sector j)
     auto src_of = [&](u32 slot, int h, int e, u32 &j, int &k) {
         if (layout == 2) {
             const u32 r = slot & 3u;
@@ -442,14 +455,24 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
             if (carry != (big ? 1 : 0)) return fail(c, HB_EINVAL, "internal: MFMA digit range");
         }
     }
-    // kz = 128 sum (r_jk mod p) + p (2^40 - 128 nneg)   (nneg <= 32 S <= 2^16)
+    // kz = 128 sum (r_jk mod p) + p (2^w - 128 nneg)   (nneg <= 32 S <= 2^16).
+    // |sum_jk r_jk u_jk| < 32 S 255 2^255 < S 2^268 < p 2^w with
+    // w = ceil(log2 S) + 14 (p > 2^255), so T = sum r u + p 2^w > 0; without
+    // the Montgomery factor (HB_MAC_MONT off) T < 2^282 for S <= 2048 and the
+    // finish is one hb_reduce_small; with it, w = 40 as before
     u64 sh = 0;
     for (int t = 0; t < 12; ++t) {   // acc *= 128
         const u64 v = (acc[t] << 7) | sh;
         sh = acc[t] >> 25;
         acc[t] = v & 0xffffffffull;
     }
-    const u64 mult = (1ull << 40) - 128ull * nneg;
+#if defined(HB_MAC_MONT)
+    const int w = 40;
+#else
+    int w = 14;
+    while ((1u << (w - 14)) < S) ++w;
+#endif
+    const u64 mult = (1ull << w) - 128ull * nneg;
     const u64 mlo = mult & 0xffffffffull, mhi = mult >> 32;
     u64 cy = 0;
     for (int t = 0; t < 12; ++t) {
@@ -460,14 +483,29 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
         cy = (u64)(s >> 32) + (plo >> 32);
     }
     for (int t = 0; t <= 2 * NL; ++t) kz[t] = t < 12 ? (u32)acc[t] : 0u;
-    for (u32 slot = 0; slot < S; ++slot)
-        for (int l = 0; l < 64; ++l)
-            for (int e = 0; e < 16; ++e) {
-                u32 j;
-                int k;
-                src_of(slot, l >> 5, e, j, k);
-                frag[((size_t)slot * 64 + l) * 16 + e] = D[((size_t)j * 32 + (size_t)k) * 32 + (l & 31)];
-            }
+    if (layout == 3) {
+        // v_mfma_i32_16x16x64_i8 A operand, tile t of K slice p (sectors
+        // 2p, 2p+1) at fragment 2p + t: lane (g, m) = (l >> 4, l & 15) byte e
+        // is A[row 16 t + m][k = 16 g + e], k = byte k % 32 of sector 2p + k / 32
+        for (u32 p = 0; p < S / 2; ++p)
+            for (int t = 0; t < 2; ++t)
+                for (int l = 0; l < 64; ++l)
+                    for (int e = 0; e < 16; ++e) {
+                        const int k = 16 * (l >> 4) + e;
+                        const u32 j = 2 * p + (u32)(k / 32);
+                        frag[((size_t)(2 * p + t) * 64 + l) * 16 + e] =
+                            D[((size_t)j * 32 + (size_t)(k % 32)) * 32 + (size_t)(16 * t + (l & 15))];
+                    }
+    } else {
+        for (u32 slot = 0; slot < S; ++slot)
+            for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < 16; ++e) {
+                    u32 j;
+                    int k;
+                    src_of(slot, l >> 5, e, j, k);
+                    frag[((size_t)slot * 64 + l) * 16 + e] = D[((size_t)j * 32 + (size_t)k) * 32 + (l & 31)];
+                }
+    }
 #else
     std::vector<int> digits((size_t)S * 33);
     Limbs sum(NL, 0);
@@ -587,12 +625,20 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         // phase's fixed cost: measured 67.2 vs 72.7 GiB/s at configs[1], S = 1)
         if (!cxx && pi.ss == 32 && S >= 4 && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
             !getenv("HB_NO_MFMA")) {
-            // whole-line sector loads when every line of 4 sectors lies in
-            // one block ($HB_MFMA_SECTOR_LOADS: the sector-shaped loads, A/B)
+            // 3: the 16x16x64 MFMA, whose B operand is the whole-line load
+            // shape (S even); 2: 32x32x32 with whole-line loads and an
+            // in-quad transpose (S % 4 == 0; $HB_MFMA_LINE32, A/B); 1:
+            // 32x32x32 with sector-shaped loads ($HB_MFMA_SECTOR_LOADS, A/B)
 #if defined(HB_NO_LINE_LOADS)
             const int layout = 1;
 #else
-            const int layout = S % 4 == 0 && !getenv("HB_MFMA_SECTOR_LOADS") ? 2 : 1;
+            const bool sector = getenv("HB_MFMA_SECTOR_LOADS") != nullptr;
+#if defined(HB_MFMA_TOEPLITZ)
+            const bool m16 = false;
+#else
+            const bool m16 = S % 2 == 0 && !sector && !getenv("HB_MFMA_LINE32");
+#endif
+            const int layout = m16 ? 3 : S % 4 == 0 && !sector ? 2 : 1;
 #endif
             rc = mfma_tables(c, p, S, A.kz, layout);
             if (rc) return rc;
