@@ -39,12 +39,10 @@ struct HbRetry {
 // A-operand tiles per sector: 1 (dense reduced digits: 32 output digits) or
 // 2 (HB_MFMA_TOEPLITZ, the A/B variant: 64 output digits of the unreduced
 // product, half of each tile zero)
-// The dense MAC's finish: HB_MAC_MONT = Montgomery REDC of T + F R (the
-// tiles carry alpha_j R); HB_MAC_PLAIN = one quotient-estimate reduction of
-// T + F (the tiles carry alpha_j).  Until measured, MONT is the default.
-#if !defined(HB_MAC_PLAIN) && !defined(HB_MAC_MONT)
-#define HB_MAC_MONT
-#endif
+// The dense MAC's finish: one quotient-estimate reduction of T + F (the
+// tiles carry alpha_j; default), or with HB_MAC_MONT (A/B variant) the
+// Montgomery REDC of T + F R (the tiles carry alpha_j R): 1,100.0 vs
+// 1,087.3 GiB/s for the plain finish
 #if defined(HB_MFMA_TOEPLITZ)
 #define HB_MFMA_NT 2
 #else
