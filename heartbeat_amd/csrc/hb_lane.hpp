@@ -389,6 +389,20 @@ HB_HD u32 hb_prf_try_from(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], c
             ++wi;
         }
     }
+#if defined(HB_UNROLL_FIRST_TRY)
+    // A/B variant: the first try's word loop unrolled (no register rotation
+    // of dq / out between words, 6x the loop's code)
+    if constexpr (FIRST != 0) {
+        HB_UNROLL
+        for (u32 k = 1; k < NL; ++k) {
+            if (wi < nw) {
+                emit(hb_cfb8_word<NR>(L, P.rk, s0, s1, s2, s3, dq[0]) & top);
+                top = 0xffffffffu;
+                ++wi;
+            }
+        }
+    }
+#endif
     HB_NOUNROLL
     for (; wi < nw; ++wi) {
         emit(hb_cfb8_word<NR>(L, P.rk, s0, s1, s2, s3, dq[0]) & top);
