@@ -383,26 +383,15 @@ HB_HD u32 hb_prf_try_from(const LaneTab &L, const PrfParams<NL> &P, u32 sr[4], c
     // constants (36 of its 788 lookups go).  Peeling word 2 as well (steps
     // 8-11: 2, 1, 1, 1 zero words, 20 more) measured slower (code size);
     // word 1 alone: +0.9 % at configs[2] (same-box A/B, profiles/r03/s3).
+    // The rest of the word loop stays rolled: unrolled (no register rotation
+    // of dq / out, 116 instead of 128 VGPRs, no scratch) it measured -1.8 %
+    // (profiles/r04/j).
     if constexpr (FIRST != 0) {
         if (wi < nw) {
             emit(hb_cfb8_word<NR, 3, 2>(L, P.rk, s0, s1, s2, s3, dq[0], P.r1z));
             ++wi;
         }
     }
-#if defined(HB_UNROLL_FIRST_TRY)
-    // A/B variant: the first try's word loop unrolled (no register rotation
-    // of dq / out between words, 6x the loop's code)
-    if constexpr (FIRST != 0) {
-        HB_UNROLL
-        for (u32 k = 1; k < NL; ++k) {
-            if (wi < nw) {
-                emit(hb_cfb8_word<NR>(L, P.rk, s0, s1, s2, s3, dq[0]) & top);
-                top = 0xffffffffu;
-                ++wi;
-            }
-        }
-    }
-#endif
     HB_NOUNROLL
     for (; wi < nw; ++wi) {
         emit(hb_cfb8_word<NR>(L, P.rk, s0, s1, s2, s3, dq[0]) & top);
