@@ -96,6 +96,10 @@ struct hb_ctx {
     DevBuf mseeds, moffs, mdig;   // Merkle chunk seeds, offsets, HMAC digests
     HostBuf gstage[2];   // host-file prove: pinned gather buffers (blocks | tags), double-buffered
     HostBuf hscratch;    // pinned staging of the encode's small host round trips (alpha, MFMA tables)
+    // the alpha D2H into hscratch done / the MFMA-table H2D out of it done
+    // (not yet waited for: the next round trip must wait before reusing hscratch)
+    hipEvent_t ev_alpha = nullptr, ev_h2d = nullptr;
+    bool h2d_pending = false;
     bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
     u32 *hres = nullptr; // pinned host copy of wsum results (+ status)
     size_t hres_n = 0;
@@ -357,12 +361,18 @@ u64 retry_capacity(const uint8_t *p_be, size_t p_len, u64 nb) {
 // j0 % 4 == 0, holds chunk 4h + r of the line of sectors j0 .. j0+3: byte
 // 16 (r % 2) + e of sector j0 + 2h + r / 2), see hb_line_loads; 3 = the
 // 16x16x64 MFMA (S % 2 == 0, dense only), see hb_mfma16_block_acc.
-int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
+// Two halves, so that the host builds the tables while the GPU runs the
+// prefix kernel: mfma_tables_begin enqueues the D2H of alpha (after the
+// alpha PRF, before the prefix kernel in stream order); mfma_tables waits for
+// that copy only, builds the tables and enqueues their H2D (after the prefix
+// kernel, before the first pass), without synchronizing the stream.
+int mfma_tables_begin(hb_ctx *c, u32 S) {
     const int NL = 8;
+    if (c->h2d_pending) {   // the previous call's H2D still reads hscratch
+        HB_CHECK(hipEventSynchronize(c->ev_h2d), "H2D(afrag)");
+        c->h2d_pending = false;
+    }
     HB_CHECK(c->hscratch.ensure((size_t)S * NL * 4 + (size_t)HB_MFMA_NT * S * 64 * 16), "hipHostMalloc(scratch)");
-    u32 *am = (u32 *)c->hscratch.p;
-    int8_t *frag = (int8_t *)c->hscratch.p + (size_t)S * NL * 4;
-    const size_t frag_bytes = (size_t)HB_MFMA_NT * S * 64 * 16;
 #if !defined(HB_MFMA_TOEPLITZ) && !defined(HB_MAC_MONT)
     // the dense tiles carry alpha_j itself (the finish adds F and reduces,
     // no REDC); HB_MAC_MONT / the Toeplitz MAC: alpha_j R mod p
@@ -370,8 +380,17 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
 #else
     const void *asrc = c->alpha_mont.p;
 #endif
-    HB_CHECK(hipMemcpyAsync(am, asrc, (size_t)S * NL * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
-    HB_CHECK(hipStreamSynchronize(c->stream), "alpha PRF");
+    HB_CHECK(hipMemcpyAsync(c->hscratch.p, asrc, (size_t)S * NL * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
+    HB_CHECK(hipEventRecord(c->ev_alpha, c->stream), "hipEventRecord");
+    return 0;
+}
+
+int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
+    const int NL = 8;
+    u32 *am = (u32 *)c->hscratch.p;
+    int8_t *frag = (int8_t *)c->hscratch.p + (size_t)S * NL * 4;
+    const size_t frag_bytes = (size_t)HB_MFMA_NT * S * 64 * 16;
+    HB_CHECK(hipEventSynchronize(c->ev_alpha), "alpha PRF");
     // layouts 1, 2 (32x32x32 B operand): slot s, lane half h, byte e ->
     // (sector j, byte k of sector j)
     auto src_of = [&](u32 slot, int h, int e, u32 &j, int &k) {
@@ -553,7 +572,8 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
 #endif
     HB_CHECK(c->afrag.ensure(frag_bytes), "hipMalloc(afrag)");
     HB_CHECK(hipMemcpyAsync(c->afrag.p, frag, frag_bytes, hipMemcpyHostToDevice, c->stream), "H2D(afrag)");
-    HB_CHECK(hipStreamSynchronize(c->stream), "H2D(afrag)");
+    HB_CHECK(hipEventRecord(c->ev_h2d, c->stream), "hipEventRecord");
+    c->h2d_pending = true;
     return 0;
 }
 
@@ -618,12 +638,16 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 
     EncodeArgs<NL> A;
     memset(&A, 0, sizeof A);
+    int mf_layout = 0;   // MFMA MAC table layout (0: VALU MAC)
     if constexpr (NL == 8) {
         // MFMA MAC tables (hb_mfma_block_acc): 256-bit primes with whole
         // 32-byte sectors, PySwizzle PRF, two-pass encode
         // (below 4 sectors per block the VALU MAC is cheaper than the MFMA
-        // phase's fixed cost: measured 67.2 vs 72.7 GiB/s at configs[1], S = 1)
-        if (!cxx && pi.ss == 32 && S >= 4 && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
+        // phase's fixed cost: at configs[1], S = 1, the m16 MFMA MAC measured
+        // 70.98 vs 71.32 GiB/s, same-box A/B, profiles/r04/l)
+        // $HB_MFMA_MIN_S: the smallest sector count given the MFMA MAC (A/B)
+        static const u32 min_s = getenv("HB_MFMA_MIN_S") ? (u32)atoi(getenv("HB_MFMA_MIN_S")) : 4u;
+        if (!cxx && pi.ss == 32 && S >= min_s && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
             !getenv("HB_NO_MFMA")) {
             // 3: the 16x16x64 MFMA, whose B operand is the whole-line load
             // shape (S even); 2: 32x32x32 with whole-line loads and an
@@ -640,13 +664,11 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 #endif
             const int layout = m16 ? 3 : S % 4 == 0 && !sector ? 2 : 1;
 #endif
-            rc = mfma_tables(c, p, S, A.kz, layout);
+            rc = mfma_tables_begin(c, S);
             if (rc) return rc;
-            A.mfma = (u32)layout;
-            A.afrag = (const u32 *)c->afrag.p;
+            mf_layout = layout;
         }
     }
-    mark("MFMA tables");
     int nr = 0;
     if (!make_prf<NL>(f_key, key_len, p_be, p_len, A.prf, nr)) return fail(c, HB_EINVAL, "invalid key");
     make_mod<NL>(p, A.mod);
@@ -704,6 +726,14 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         PA.out = (unsigned char *)c->pfx.p;
         HB_CHECK(hb_launch_prefix(PA, nr, c->num_cus, c->stream), "hb_prefix_kernel launch");
         c->last_launches++;
+    }
+    if (mf_layout) {
+        // built on the host while the GPU runs the prefix kernel
+        rc = mfma_tables(c, p, S, A.kz, mf_layout);
+        if (rc) return rc;
+        A.mfma = (u32)mf_layout;
+        A.afrag = (const u32 *)c->afrag.p;
+        mark("MFMA tables");
     }
 
     auto launch = [&](const uint8_t *d, u64 dlen, u64 nb, u64 base, uint8_t *tg) -> int {
@@ -1256,6 +1286,8 @@ int hb_ctx_create(int device, hb_ctx **out) {
         if ((e = hipEventCreateWithFlags(&c->copied[b], hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
         if ((e = hipEventCreateWithFlags(&c->done[b], hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     }
+    if ((e = hipEventCreateWithFlags(&c->ev_alpha, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&c->ev_h2d, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipMalloc(&c->t0, 256 * sizeof(u32))) != hipSuccess) return bad(e, "hipMalloc");
     if ((e = hipMemcpy(c->t0, aes_tables().t0, 256 * sizeof(u32), hipMemcpyHostToDevice)) != hipSuccess)
         return bad(e, "hipMemcpy");
@@ -1286,6 +1318,8 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->queue) (void)hipFree(c->queue);
     if (c->k0) (void)hipEventDestroy(c->k0);
     if (c->k1) (void)hipEventDestroy(c->k1);
+    if (c->ev_alpha) (void)hipEventDestroy(c->ev_alpha);
+    if (c->ev_h2d) (void)hipEventDestroy(c->ev_h2d);
     for (int b = 0; b < 2; ++b) {
         if (c->copied[b]) (void)hipEventDestroy(c->copied[b]);
         if (c->done[b]) (void)hipEventDestroy(c->done[b]);
