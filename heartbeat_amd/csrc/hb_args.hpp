@@ -26,11 +26,22 @@
 // (relative to the launch) and the CFB-8 shift register after that try.
 // With the MFMA MAC (EncodeArgs::mfma) the first pass has already computed
 // the block's sum_j alpha_j m_ij mod p: `part`, so the retry pass only adds F.
+// HB_RETRY_DIGEST: evals whose first try is rejected by its first output
+// word (all but ~2^-32 of them) are listed before the try with the SHA-256
+// digest of their index (flags bit 0), which the retry pass then reads
+// instead of recomputing it.
+#ifndef HB_RETRY_DIGEST
+#define HB_RETRY_DIGEST 0
+#endif
 struct HbRetry {
     u64 blk;
-    u64 pad_;
+    u32 flags;
+    u32 pad_;
     u32 sr[4];
     u32 part[8];
+#if HB_RETRY_DIGEST
+    u32 dig[8];
+#endif
 };
 
 // MFMA MAC (hb_mfma_block_acc): the 256-bit sector MAC as an int8 matrix
@@ -68,6 +79,7 @@ struct EncodeArgs {
     HbRetry *retry;               // retry list (two-pass encode)
     unsigned long long *retry_count;
     u64 retry_cap;
+    u32 rtop;                     // top 32 bits of R (= p) in the PRF's nb-byte frame
     // MFMA MAC (256-bit primes, 32-byte aligned sectors): A-operand fragments
     // ([HB_MFMA_NT][S][64 lanes][16 B]) and the constant kz (hb_runtime.cpp,
     // mfma_tables): the 32 signed base-256 digits of r_jk = alpha_j 256^(31-k)

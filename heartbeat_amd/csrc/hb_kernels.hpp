@@ -787,40 +787,74 @@ __device__ __forceinline__ void hb_finish_T(u32 T[2 * NL + 1], const u32 F[NL], 
 // (T + F') mod p with F' = F (accepted) or 0 (rejected) (hb_finish_T): with ~14 %
 // rejected first tries nearly every wave has lanes of both kinds, and two
 // divergent reductions would cost both per wave.
+// HB_RETRY_DIGEST: list the lanes of `mask` (first output word above R's top
+// word: rejected whatever the try's other bytes are) with their digest, before
+// the try; `base` = the wave's first slot.
+template <int NL>
+__device__ __forceinline__ void hb_list_early(const EncodeArgs<NL> &A, u64 job, u64 mask, const u32 dig[8],
+                                              u64 &base) {
+#if HB_RETRY_DIGEST
+    u64 b = 0;
+    if (hb_lane_id() == 0) b = atomicAdd(A.retry_count, (unsigned long long)__popcll(mask));
+    base = hb_bcast64(b);
+    if ((mask >> hb_lane_id()) & 1ull) {
+        const u64 slot = base + hb_mbcnt(mask);
+        if (slot < A.retry_cap) {
+            HbRetry *e = A.retry + slot;
+            *reinterpret_cast<uint4 *>(e) = make_uint4((u32)job, (u32)(job >> 32), 1u, 0u);
+            *reinterpret_cast<uint4 *>(e->dig) = make_uint4(dig[0], dig[1], dig[2], dig[3]);
+            *reinterpret_cast<uint4 *>(e->dig + 4) = make_uint4(dig[4], dig[5], dig[6], dig[7]);
+        }
+    }
+#endif
+}
+
 template <int NL, int NR, int ALIGN, class H>
 __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const LaneTab &L, H &h, u64 job,
                                                 bool active, u32 ok, u32 sr[4], u32 out[NL], u32 &tries,
-                                                u32 &failed, u32 *T, bool tmine) {
+                                                u32 &failed, u32 *T, bool tmine, u64 pre_base, u64 pre_mask) {
     tries += active ? 1u : 0u;
     const bool rejected = active && !ok;
-    const u64 rej = __ballot(rejected);
+    // listed before the try (hb_list_early; always rejected)
+    const bool pre = (pre_mask >> hb_lane_id()) & 1ull;
+    const u64 rej = __ballot(rejected && !pre);
     bool listed = false;
     HbRetry *e = nullptr;
+    if (pre) {
+        const u64 slot = pre_base + hb_mbcnt(pre_mask);
+        if (slot < A.retry_cap) {
+            listed = true;
+            e = A.retry + slot;
+        }
+    }
     if (rej) {
         u64 base = 0;
         if (hb_lane_id() == 0) base = atomicAdd(A.retry_count, (unsigned long long)__popcll(rej));
         base = hb_bcast64(base);
-        if (rejected) {
+        if (rejected && !pre) {
             const u64 slot = base + hb_mbcnt(rej);
             if (slot < A.retry_cap) {
                 listed = true;
                 e = A.retry + slot;
-                e->blk = job;
-                *reinterpret_cast<uint4 *>(e->sr) = make_uint4(sr[0], sr[1], sr[2], sr[3]);
-            } else {
-                // retry list full (never at its sizing, see hb_runtime.cpp):
-                // finish this eval in place
-                u32 dig[8];
-                hb_sha256_decimal(A.block_base + job, dig);
-                u32 n = 1;
-                while (!ok && n < HB_MAX_TRIES) {
-                    ok = hb_prf_try<NL, NR>(L, A.prf, sr, dig, out);
-                    ++n;
-                    ++tries;
-                }
-                failed += ok ? 0u : 1u;
+                // no digest stored (flags 0): the retry pass hashes the index
+                *reinterpret_cast<uint4 *>(e) = make_uint4((u32)job, (u32)(job >> 32), 0u, 0u);
             }
         }
+    }
+    if (listed) {
+        *reinterpret_cast<uint4 *>(e->sr) = make_uint4(sr[0], sr[1], sr[2], sr[3]);
+    } else if (rejected) {
+        // retry list full (never at its sizing, see hb_runtime.cpp): finish
+        // this eval in place
+        u32 dig[8];
+        hb_sha256_decimal(A.block_base + job, dig);
+        u32 n = 1;
+        while (!ok && n < HB_MAX_TRIES) {
+            ok = hb_prf_try<NL, NR>(L, A.prf, sr, dig, out);
+            ++n;
+            ++tries;
+        }
+        failed += ok ? 0u : 1u;
     }
     const bool done = active && ok;
 #if defined(HB_EXP_NO_FINISH)   // instruction-count experiment only (wrong tags)
@@ -901,17 +935,26 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_fi
             else if (A.mfma) tmine = hb_mfma_block_acc<NL, false>(A, afl_glb, job, act, T);
         }
         u32 out[NL], sr[4], ok;
+        u64 pre_base = 0, pre_mask = 0;
         {
             u32 dig[8];
             hb_sha256_decimal(A.block_base + job, dig);
+            hb_prf_prefix<NL>(A.pfx, A.o0, A.prf, dig[0], sr, out);
+#if HB_RETRY_DIGEST
+            // the first output word alone decides all but ~2^-32 of the
+            // rejections: list those evals now, while their digest is live
+            pre_mask = __ballot(act && out[0] > A.rtop);
+            if (pre_mask) hb_list_early<NL>(A, job, pre_mask, dig, pre_base);
+#endif
             // waves in their AES phase go first in issue arbitration, so the
             // LDS stays fed while other waves hash or run the MAC (+0.8 %,
             // same-box A/B, profiles/r02/s13)
             __builtin_amdgcn_s_setprio(HB_AES_PRIO);
-            ok = hb_prf_first_try<NL, NR>(L, A.prf, A.pfx, A.o0, sr, dig, out);
+            ok = hb_prf_try_from<NL, NR, 1>(L, A.prf, sr, dig, out);
             __builtin_amdgcn_s_setprio(0);
         }
-        hb_first_finish<NL, NR, ALIGN>(A, L, h, job, act, ok, sr, out, tries, failed, T, tmine);
+        hb_first_finish<NL, NR, ALIGN>(A, L, h, job, act, ok, sr, out, tries, failed, T, tmine, pre_base,
+                                       pre_mask);
     }
     for (int off = 32; off > 0; off >>= 1) {
         tries += __shfl_xor(tries, off);
@@ -930,6 +973,17 @@ struct RetryHandler {
         const uint4 v = *reinterpret_cast<const uint4 *>(A.retry[job].sr);
         sr[0] = v.x; sr[1] = v.y; sr[2] = v.z; sr[3] = v.w;
     }
+#if HB_RETRY_DIGEST
+    // the digest the first pass stored (flags bit 0), else hash the index
+    __device__ __forceinline__ bool digest(u64 job, u32 dig[8]) const {
+        const HbRetry &r = A.retry[job];
+        if (!(r.flags & 1u)) return false;
+        const uint4 a = *reinterpret_cast<const uint4 *>(r.dig), b = *reinterpret_cast<const uint4 *>(r.dig + 4);
+        dig[0] = a.x; dig[1] = a.y; dig[2] = a.z; dig[3] = a.w;
+        dig[4] = b.x; dig[5] = b.y; dig[6] = b.z; dig[7] = b.w;
+        return true;
+    }
+#endif
     __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
         const u64 blk = A.retry[job].blk;
         u32 tag[NL];

@@ -17,8 +17,10 @@
 
 #if defined(__HIP__)
 #define HB_HD __device__ __forceinline__
+#define HB_HHD __host__ __device__ inline
 #else
 #define HB_HD static inline
+#define HB_HHD static inline
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -579,6 +581,19 @@ HB_HD void hb_prf_prefix(const unsigned char *pfx, u32 o0, const PrfParams<NL> &
     sr[0] = sr[1] = sr[2] = 0;
     sr[3] = x | (c3 << 24);
     out[0] = ((c0 & P.topmask) << 24) | (c1 << 16) | (c2 << 8) | c3;
+}
+
+// Top 32 bits of R in the nb-byte frame of a PRF output (P.nb >= 4).  A try
+// whose first output word (hb_prf_prefix's out[0], top byte masked) exceeds it
+// is rejected whatever its other bytes are: out >= out[0] 2^(8nb-32) >
+// (top + 1) 2^(8nb-32) - 1 >= R.  (The encode's early retry listing,
+// HB_RETRY_DIGEST; checked by tests/emul.)
+template <int NL>
+HB_HHD u32 hb_range_top(const PrfParams<NL> &P) {
+    const u32 sh = 8 * P.nb - 32, wi = sh / 32, off = sh % 32;
+    u32 top = P.R[wi] >> off;
+    if (off && wi + 1 < (u32)NL) top |= P.R[wi + 1] << (32 - off);
+    return top;
 }
 
 // The first try of a fresh eval through the prefix image (P.nb >= 4).

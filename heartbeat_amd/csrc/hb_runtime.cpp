@@ -672,6 +672,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     int nr = 0;
     if (!make_prf<NL>(f_key, key_len, p_be, p_len, A.prf, nr)) return fail(c, HB_EINVAL, "invalid key");
     make_mod<NL>(p, A.mod);
+    if (A.prf.nb >= 4) A.rtop = hb_range_top<NL>(A.prf);
     A.alpha_mont = (const u32 *)c->alpha_mont.p;
     A.t0 = c->t0;
     A.C = C;

@@ -132,9 +132,14 @@ static int prf_eval(const LaneTab &L, const PrfParams<NL> &P, int nr, uint64_t x
         if (tries == 1 && pfx && P.nb >= 4) {
             pfx->need(dig[0]);
             const unsigned char *img = pfx->img.data();
-            if (nr == 10) ok = hb_prf_first_try<NL, 10>(L, P, img, pfx->o0, sr, dig, out);
-            else if (nr == 12) ok = hb_prf_first_try<NL, 12>(L, P, img, pfx->o0, sr, dig, out);
-            else ok = hb_prf_first_try<NL, 14>(L, P, img, pfx->o0, sr, dig, out);
+            // as hb_encode_first_kernel: the prefix steps, the early-listing
+            // decision (HB_RETRY_DIGEST), then the rest of the try
+            hb_prf_prefix<NL>(img, pfx->o0, P, dig[0], sr, out);
+            const bool early_reject = out[0] > hb_range_top<NL>(P);
+            if (nr == 10) ok = hb_prf_try_from<NL, 10, 1>(L, P, sr, dig, out);
+            else if (nr == 12) ok = hb_prf_try_from<NL, 12, 1>(L, P, sr, dig, out);
+            else ok = hb_prf_try_from<NL, 14, 1>(L, P, sr, dig, out);
+            if (early_reject && ok) return -2;   // the early listing's premise broken
         } else if (nr == 10) ok = hb_prf_try<NL, 10>(L, P, sr, dig, out);
         else if (nr == 12) ok = hb_prf_try<NL, 12>(L, P, sr, dig, out);
         else ok = hb_prf_try<NL, 14>(L, P, sr, dig, out);
@@ -191,6 +196,47 @@ extern "C" int emul_prf(const uint8_t *key, size_t keylen, const uint8_t *range_
     if (bits <= 256) return emul_prf_t<8>(key, keylen, range_be, rlen, x, out_be, lane, use_prefix);
     if (bits <= 512) return emul_prf_t<16>(key, keylen, range_be, rlen, x, out_be, lane, use_prefix);
     if (bits <= 1024) return emul_prf_t<32>(key, keylen, range_be, rlen, x, out_be, lane, use_prefix);
+    return -2;
+}
+
+// The encode's early retry listing (HB_RETRY_DIGEST) over n evals x0..x0+n-1:
+// counts[0] first tries rejected, [1] of them decided by the first output
+// word alone (listed early), [2] early decisions that the full try
+// contradicted (must be 0).
+template <int NL>
+static int emul_early_t(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen, uint64_t x0,
+                        uint64_t n, uint64_t *counts) {
+    PrfParams<NL> P;
+    int nr;
+    if (!make_prf<NL>(key, keylen, range_be, rlen, P, nr) || P.nb < 4) return -1;
+    LaneTab L = make_tab(0);
+    Prefix *pfx = prefix_for(key, keylen);
+    const u32 top = hb_range_top<NL>(P);
+    counts[0] = counts[1] = counts[2] = 0;
+    for (uint64_t x = x0; x < x0 + n; ++x) {
+        uint32_t dig[8], sr[4], out[NL];
+        hb_sha256_decimal(x, dig);
+        pfx->need(dig[0]);
+        hb_prf_prefix<NL>(pfx->img.data(), pfx->o0, P, dig[0], sr, out);
+        const bool early = out[0] > top;
+        uint32_t ok;
+        if (nr == 10) ok = hb_prf_try_from<NL, 10, 1>(L, P, sr, dig, out);
+        else if (nr == 12) ok = hb_prf_try_from<NL, 12, 1>(L, P, sr, dig, out);
+        else ok = hb_prf_try_from<NL, 14, 1>(L, P, sr, dig, out);
+        counts[0] += ok ? 0 : 1;
+        counts[1] += early ? 1 : 0;
+        counts[2] += early && ok ? 1 : 0;
+    }
+    return 0;
+}
+
+extern "C" int emul_early(const uint8_t *key, size_t keylen, const uint8_t *range_be, size_t rlen, uint64_t x0,
+                          uint64_t n, uint64_t *counts) {
+    int bits = bitlen_be(range_be, rlen);
+    if (bits <= 64) return emul_early_t<2>(key, keylen, range_be, rlen, x0, n, counts);
+    if (bits <= 256) return emul_early_t<8>(key, keylen, range_be, rlen, x0, n, counts);
+    if (bits <= 512) return emul_early_t<16>(key, keylen, range_be, rlen, x0, n, counts);
+    if (bits <= 1024) return emul_early_t<32>(key, keylen, range_be, rlen, x0, n, counts);
     return -2;
 }
 

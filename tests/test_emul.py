@@ -24,6 +24,8 @@ def emul():
                               c.c_size_t, c.c_uint64, c.c_char_p, c.c_uint64, c.c_uint64,
                               c.c_char_p, c.c_int, c.c_int, c.c_int]
     L.emul_prefix_check.argtypes = [c.c_char_p, c.c_size_t, c.c_uint32, c.c_int]
+    L.emul_early.argtypes = [c.c_char_p, c.c_size_t, c.c_char_p, c.c_size_t, c.c_uint64, c.c_uint64,
+                             c.POINTER(c.c_uint64)]
     return L
 
 
@@ -129,3 +131,24 @@ def test_merkle_lane_matches_reference(emul):
             lane += 3
             assert tries >= 1
             assert dg.raw.hex() == leaf, (c["file"], c["chunksz"], sd)
+
+
+@pytest.mark.parametrize("bits,x0", [(256, 0), (256, 123456789), (255, 10**12), (250, 77), (61, 5), (512, 1000)])
+def test_early_retry_listing_premise(emul, bits, x0):
+    """The first pass lists an eval for the retry pass before its first try
+    when the try's first output word (from the prefix image) exceeds R's top
+    32 bits (hb_range_top, HB_RETRY_DIGEST): such a try must always be
+    rejected, and the rule must catch nearly every rejection."""
+    import random
+    rng = random.Random(bits * 1000003 + x0)
+    key = bytes(rng.randrange(256) for _ in range(32))
+    # a range whose top byte leaves room for rejections (like the bench prime)
+    r = rng.randrange(1 << (bits - 1), (1 << bits) - (1 << (bits - 3)))
+    counts = (ctypes.c_uint64 * 3)()
+    n = 20000
+    assert emul.emul_early(key, len(key), _be(r), len(_be(r)), x0, n, counts) == 0
+    rejected, early, wrong = counts[0], counts[1], counts[2]
+    assert wrong == 0
+    assert early <= rejected
+    assert rejected > n // 50
+    assert early >= rejected - 2, (rejected, early)
