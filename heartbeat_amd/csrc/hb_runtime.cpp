@@ -673,6 +673,9 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     if (!make_prf<NL>(f_key, key_len, p_be, p_len, A.prf, nr)) return fail(c, HB_EINVAL, "invalid key");
     make_mod<NL>(p, A.mod);
     if (A.prf.nb >= 4) A.rtop = hb_range_top<NL>(A.prf);
+    // test hook: no early retry listing (every rejected first try is listed
+    // after the try without its digest, and the retry pass hashes the index)
+    if (getenv("HB_TEST_NO_EARLY_LIST")) A.rtop = 0xffffffffu;
     A.alpha_mont = (const u32 *)c->alpha_mont.p;
     A.t0 = c->t0;
     A.C = C;

@@ -365,6 +365,37 @@ def test_two_pass_retry_list_overflow(nat, monkeypatch):
         t2.free()
 
 
+def test_retry_list_late_entries(nat, oracle, monkeypatch):
+    """Retry-list entries without a stored digest (listed after the first try,
+    flags 0: the first output word equal to R's top word, ~2^-32 of the
+    rejections, forced for all of them by HB_TEST_NO_EARLY_LIST) are hashed by
+    the retry pass: tags == the default path (early entries with digests) ==
+    the oracle, with a full and an overflowing retry list."""
+    p = int(json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))["p256"], 16)
+    S, L = 16, 6 << 20
+    nb = L // (32 * S) + 1
+    buf = DevBuf(nat, L)
+    tags = [DevBuf(nat, nb * 32) for _ in range(3)]
+    try:
+        ctx = nat.context()
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 91))
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, tags[0].p, block_base=987654321)
+        monkeypatch.setenv("HB_TEST_NO_EARLY_LIST", "1")
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, tags[1].p, block_base=987654321)
+        monkeypatch.setenv("HB_TEST_RETRY_CAP", "500")
+        dev_encode(nat, p, S, b"f" * 32, b"a" * 32, buf.p, L, nb, tags[2].p, block_base=987654321)
+        t0 = tags[0].download()
+        assert tags[1].download() == t0
+        assert tags[2].download() == t0
+        data = buf.download()
+        want = oracle.encode(p, S, b"f" * 32, b"a" * 32, data, block_base=987654321, nblocks=600)
+        assert split_tags(t0[: 600 * 32], 32) == want
+    finally:
+        buf.free()
+        for t in tags:
+            t.free()
+
+
 def test_shards_concatenate(nat):
     """Block-range shards with awkward boundaries == one whole-file launch."""
     p, S = P256, 16
