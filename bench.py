@@ -99,8 +99,11 @@ def parse(argv=None):
     ap.add_argument("--prf", default="pyswizzle", choices=["pyswizzle", "cxx"],
                     help="pyswizzle: KeyedPRF, tags bit-exact vs PySwizzle (the headline); cxx: the "
                          "cxx Swizzle extension's PRF (cxx/prf.hxx, CFB-128), parity unpinned")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the host-memory path rows (4 GiB prefix, after the CPU rows; on by default "
+                         "for the N = 1 configs[2] run)")
     ap.add_argument("--host-path", action="store_true",
-                    help="also time the pinned/pageable host path on a 4 GiB prefix (DESIGN.md)")
+                    help="time the host-memory path rows in any configuration")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the launch / rank / timing / JSON plumbing without HIP calls (CPU tests)")
     args = ap.parse_args(argv)
@@ -453,6 +456,7 @@ def bench_encode(args, cfg, R):
             },
         },
         "context_prepare_ms": round(prepare_ms, 2),   # hb_ctx_prepare, before the timed region
+        "build": _native.build_info(),   # provenance of libhbswizzle.so (hb_build_id, checked against the tree)
         "prf_tries_per_block": round(tries_per_block, 4),
         "aes_per_block": round(aes / nblocks, 3),
     }
@@ -469,8 +473,13 @@ def bench_encode(args, cfg, R):
             fill(0)
         line["cpu_baseline"] = cpu_baseline(ctx, L, dptr, tptr, pieces[0][1], S, p, fk, ak, C,
                                             args.cpu_seconds, args.cpu_threads, args.py_seconds, cxx)
-    if R.rank == 0 and args.host_path:
+    want_host = args.host_path or (R.world == 1 and args.config == "c3" and not cxx and not args.single_pass)
+    if R.rank == 0 and want_host and not args.no_host_path:
+        t = time.perf_counter()
+        if len(pieces) > 1:
+            fill(0)
         line["host_path"] = host_path(ctx, L, dptr, pieces[0][1], S, pb, fk, ak, C)
+        line["host_path"]["seconds_spent"] = round(time.perf_counter() - t, 1)
 
     if R.rank == 0:
         print(json.dumps(line), flush=True)
@@ -731,9 +740,23 @@ def host_file_prove(ctx, L, dptr, pys, p, S, path, n, tag):
 
 def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
     """Rate with the file and the tags in host memory (the boundary of a
-    file-like object in, tag bytes out): chunked H2D of sectors + encode + D2H
-    of tags, all inside the timed region, once from a pageable buffer and once
-    from the same buffer page-locked with hb_host_register (pinned DMA)."""
+    file-like object in, tag bytes out; north_star: "the rate including pinned
+    hipMemcpyAsync of sectors in and tags out"): chunked H2D of sectors +
+    encode + D2H of tags, all inside the timed region, on a 4 GiB prefix of
+    the same synthetic file.  Never `value`.  Rows:
+      raw_*: hb_encode on a host buffer -- pageable (the runtime's staging),
+        page-locked read-only in 256 MiB windows by the library itself
+        (HB_HOST_REGISTER, registration inside the timed call), and pinned
+        beforehand by the caller (hb_host_register, registration not timed);
+      api_*: the drop-in API (PySwizzle.py:279-314 -> encode_file) on a BytesIO
+        (its buffer, zero copy) and on a real file (read-only mmap, page cache
+        warm), each with and without the windowed registration; `api_default`
+        names what encode_file does by itself (REGISTER_KINDS);
+      api_prove_file: PySwizzle.prove on the real file, default challenge.
+    Every run's tags are compared with the first one's."""
+    import importlib
+    import io
+    import tempfile
     import numpy as np
     n = min(length, 4 * GIB) // C * C
     host = np.empty(n, dtype=np.uint8)
@@ -741,56 +764,72 @@ def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
     nb = n // C
     tags = np.empty(nb * 32, dtype=np.uint8)
     ref = np.empty(nb * 32, dtype=np.uint8)
-    out = {"bytes": n, "chunk": "256 MiB of whole blocks, double-buffered, H2D / D2H on a copy stream"}
+    out = {"bytes": n, "chunk": "256 MiB of whole blocks, double-buffered, H2D / D2H on a copy stream",
+           "note": "PCIe-inclusive rates of the host-memory boundary; never `value` (DESIGN.md 6)"}
 
-    def run(dst):
+    def run(dst, flags=0):
         t = time.perf_counter()
         ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, host.ctypes.data, n, nb,
-                              dst.ctypes.data, 0, None))
+                              dst.ctypes.data, flags, None))
         return time.perf_counter() - t
 
     run(ref)   # warm-up (staging buffers, prefix image allocation)
-    out["pageable_gib_s"] = round(n / GIB / run(tags), 3)
+    out["raw_pageable_gib_s"] = round(n / GIB / run(tags), 3)
     ok = bool(np.array_equal(tags, ref))
+    run(tags, _native_flag("HB_HOST_REGISTER"))
+    out["raw_register_windows_gib_s"] = round(n / GIB / run(tags, _native_flag("HB_HOST_REGISTER")), 3)
+    ok = ok and bool(np.array_equal(tags, ref))
     ctx.check(L.hb_host_register(ctx.h, host.ctypes.data, n))
     ctx.check(L.hb_host_register(ctx.h, tags.ctypes.data, tags.nbytes))
     try:
         run(tags)
-        out["pinned_gib_s"] = round(n / GIB / run(tags), 3)
+        out["raw_pinned_gib_s"] = round(n / GIB / run(tags), 3)
         ok = ok and bool(np.array_equal(tags, ref))
     finally:
         ctx.check(L.hb_host_unregister(ctx.h, tags.ctypes.data))
         ctx.check(L.hb_host_unregister(ctx.h, host.ctypes.data))
-    out["pinned_tags_equal_pageable"] = ok
-    # the same bytes through the drop-in API (PySwizzle.py:279-314 ->
-    # heartbeat_amd.PySwizzle.encode_file): a BytesIO (its buffer, zero-copy)
-    # and a real file (read-only mmap, page cache warm), default device set
-    import importlib
-    import io
-    import tempfile
+    out["raw_tags_equal"] = ok
     pys = importlib.import_module("heartbeat_amd.PySwizzle.PySwizzle")
     p = int.from_bytes(pb, "big")
+    out["api_default"] = {"register_kinds": list(pys.REGISTER_KINDS)}
+
+    def api(src, register, reps=2):
+        best = None
+        for _ in range(reps):
+            src.seek(0)
+            t = time.perf_counter()
+            tag, _ = pys.encode_file(p, S, fk, ak, src, register=register)
+            dt = time.perf_counter() - t
+            best = dt if best is None else min(best, dt)
+        return n / GIB / best, tag._raw[:nb * 32] == ref.tobytes()
+
+    api_ok = True
     bio = io.BytesIO(host.tobytes())
     pys.encode_file(p, S, fk, ak, bio)          # warm-up
-    bio.seek(0)
-    t = time.perf_counter()
-    tag, _ = pys.encode_file(p, S, fk, ak, bio)
-    out["api_bytesio_gib_s"] = round(n / GIB / (time.perf_counter() - t), 3)
-    ok = ok and tag._raw[:nb * 32] == ref.tobytes()
-    del bio, tag
+    for reg, key in ((False, "api_bytesio_gib_s"), (True, "api_bytesio_register_gib_s")):
+        r, same = api(bio, reg)
+        out[key] = round(r, 3)
+        api_ok = api_ok and same
+    del bio
     with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp")) as fh:
         host.tofile(fh.name)
         with open(fh.name, "rb") as f:
             pys.encode_file(p, S, fk, ak, f)
+            for reg, key in ((False, "api_file_mmap_gib_s"), (True, "api_file_mmap_register_gib_s")):
+                r, same = api(f, reg)
+                out[key] = round(r, 3)
+                api_ok = api_ok and same
             f.seek(0)
-            t = time.perf_counter()
             tag, _ = pys.encode_file(p, S, fk, ak, f)
-            out["api_file_mmap_gib_s"] = round(n / GIB / (time.perf_counter() - t), 3)
-        ok = ok and tag._raw[:nb * 32] == ref.tobytes()
         out["api_prove_file"] = host_file_prove(ctx, L, dptr, pys, p, S, fh.name, n, tag)
-    out["api_tags_equal"] = ok
+    out["api_tags_equal"] = api_ok
     out["unit"] = "GiB/s"
     return out
+
+
+def _native_flag(name):
+    from heartbeat_amd import _native
+    return getattr(_native, name)
 
 
 def bench_prove(args, cfg, R):
@@ -848,6 +887,7 @@ def bench_prove(args, cfg, R):
                    "sectors": S, "prime_bits": 256, "chunks": chunks,
                    "prf": "cxx prf, cxx prove (parity unpinned)" if cxx else "PySwizzle KeyedPRF"},
         "gathered_bytes_per_proof": chunks * (C + w),
+        "build": _native.build_info(),
     }
     if R.rank == 0 and not args.no_cpu_baseline and not cxx:
         import numpy as np

@@ -361,10 +361,19 @@ class PySwizzle(object):
         return Proof
 
 
-def encode_file(p, sectors, f_key, alpha_key, file, devices=None):
+# Host buffers whose bytes hb_encode page-locks read-only in windows
+# (HB_HOST_REGISTER) instead of staging them through the runtime's pageable
+# copies, by FileBuffer kind; bench.py's host_path measures both ways
+# (DESIGN.md 6).
+REGISTER_KINDS = ()
+
+
+def encode_file(p, sectors, f_key, alpha_key, file, devices=None, register=None):
     """GPU encode of a file object / buffer: (Tag, number of blocks).  Files of
     at least 2 x multi.MIN_SHARD_BYTES are sharded by block range over
-    `devices` (default: multi.devices(), every visible GPU)."""
+    `devices` (default: multi.devices(), every visible GPU).  `register`
+    forces (True) or forbids (False) the windowed read-only page-locking of
+    the host bytes (HB_HOST_REGISTER); None: REGISTER_KINDS decides."""
     w = _native.width_of(p)
     ss = p.bit_length() // 8
     C = ss * sectors
@@ -377,8 +386,9 @@ def encode_file(p, sectors, f_key, alpha_key, file, devices=None):
         # the tags land in the array the Tag keeps: no zero fill, no copy of
         # the image (a bytes-like buffer to Tag)
         out = np.empty(nblocks * w, dtype=np.uint8)
-        multi.encode_shards(p, sectors, fk, ak, fb.addr, fb.len, nblocks, out.ctypes.data, 0,
-                            multi.devices(devices))
+        reg = fb.kind in REGISTER_KINDS if register is None else bool(register)
+        multi.encode_shards(p, sectors, fk, ak, fb.addr, fb.len, nblocks, out.ctypes.data,
+                            _native.HB_HOST_REGISTER if reg else 0, multi.devices(devices))
         fb.consume()
     finally:
         fb.close()

@@ -53,10 +53,15 @@ class FileBuffer(object):
         start = 0 if from_start else pos
         self.start = start
         arr = None
+        # where the bytes live: "bytesio" / "bytes" (the caller's buffer),
+        # "mmap" (a read-only mapping of a real file), "read" (one read() copy)
+        self.kind = "read"
         if isinstance(file, io.BytesIO):
             arr = np.frombuffer(file.getbuffer(), dtype=np.uint8)[start:]
+            self.kind = "bytesio"
         elif isinstance(file, (bytes, bytearray, memoryview)):
             arr = np.frombuffer(file, dtype=np.uint8)
+            self.kind = "bytes"
         else:
             fd = None
             try:
@@ -76,6 +81,7 @@ class FileBuffer(object):
                             flags |= mmap.MAP_POPULATE
                         self._mm = mmap.mmap(fd, 0, flags=flags, prot=mmap.PROT_READ)
                         arr = np.frombuffer(self._mm, dtype=np.uint8)[start:]
+                        self.kind = "mmap"
                     else:
                         arr = np.zeros(0, dtype=np.uint8)
                 except (OSError, ValueError):

@@ -21,7 +21,9 @@ HB_ENCODE_SINGLE_PASS = 4
 HB_EUNSUPPORTED = -4
 HB_PRF_CXX = 8
 HB_ASYNC = 16
+HB_HOST_REGISTER = 32
 HB_BUILD_EXPERIMENT = 1
+HB_BUILD_TEST_SWITCHES = 2
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -35,6 +37,9 @@ _B = _c.c_char_p
 SIGNATURES = [
     ("hb_abi_version", _c.c_int, []),
     ("hb_build_flags", _c.c_int, []),
+    ("hb_build_id", _c.c_char_p, []),
+    ("hb_build_flags_string", _c.c_char_p, []),
+    ("hb_test_switches", _c.c_uint32, []),
     ("hb_device_count", _c.c_int, [_c.POINTER(_c.c_int)]),
     ("hb_device_pci_bus_id", _c.c_int, [_c.c_int, _P, _c.c_size_t]),
     ("hb_ctx_create", _c.c_int, [_c.c_int, _c.POINTER(_P)]),
@@ -78,6 +83,9 @@ SIGNATURES = [
 ]
 
 
+_PROVENANCE = ("hb_build_id", "hb_build_flags_string", "hb_test_switches")
+
+
 def lib():
     """The loaded library (raises HeartbeatError if it was not built)."""
     global _lib
@@ -90,17 +98,47 @@ def lib():
                     "libhbswizzle.so is not built (%s); run heartbeat_amd.build.build()" % LIB_PATH)
             L = ctypes.CDLL(LIB_PATH)
             for name, res, args in SIGNATURES:
-                if os.environ.get("HB_LIB_PATH") and not hasattr(L, name):
-                    continue   # an A/B experiment build from before this entry point
+                if not hasattr(L, name) and (os.environ.get("HB_LIB_PATH") or name in _PROVENANCE):
+                    continue   # an A/B experiment build from before this entry point, or a
+                               # library without provenance (refused by check_build_id)
                 f = getattr(L, name)
                 f.restype = res
                 f.argtypes = args
             flags = L.hb_build_flags() if hasattr(L, "hb_build_flags") else 0
-            if flags & HB_BUILD_EXPERIMENT and not os.environ.get("HB_LIB_PATH"):
-                raise HeartbeatError("%s is an experiment build (HB_EXP_* switches may emit wrong "
-                                     "tags); rebuild the product library" % LIB_PATH)
+            if not os.environ.get("HB_LIB_PATH"):
+                if flags & HB_BUILD_EXPERIMENT:
+                    raise HeartbeatError("%s is an experiment build (HB_EXP_* switches may emit wrong "
+                                         "tags); rebuild the product library" % LIB_PATH)
+                check_build_id(L)
             _lib = L
     return _lib
+
+
+def check_build_id(L, root=None):
+    """Refuse a library that was not built from the sources of the tree at
+    `root` (default: the tree this package sits in): its hb_build_id() must
+    equal build_id.library_id(SHA-256 of the tree's csrc/ + include/hbswizzle.h,
+    the library's compiler flags).  Content hashes, so a touched but unchanged
+    tree still matches, and a stale or hand-restored binary does not.  Returns
+    the id."""
+    from . import build_id as B
+    if not hasattr(L, "hb_build_id"):
+        raise HeartbeatError("%s has no build id (built before provenance stamping); rebuild it" % LIB_PATH)
+    got = L.hb_build_id().decode("ascii", "replace")
+    want = B.library_id(B.sources_digest(root), L.hb_build_flags_string().decode("ascii", "replace"))
+    if got != want:
+        raise HeartbeatError("%s was built from other sources than the tree at %s (library id %s, tree %s); "
+                             "rebuild it (heartbeat_amd.build.build())" % (
+                                 LIB_PATH, root or os.path.dirname(HERE), got[:16], want[:16]))
+    return got
+
+
+def build_info():
+    """Provenance of the loaded library, for bench lines and smoke()."""
+    L = lib()
+    return {"build_id": L.hb_build_id().decode("ascii", "replace") if hasattr(L, "hb_build_id") else None,
+            "build_flags": int(L.hb_build_flags()),
+            "test_switches": int(L.hb_test_switches()) if hasattr(L, "hb_test_switches") else None}
 
 
 def pci_bus_id(device):

@@ -4,6 +4,10 @@
 #pragma once
 #include "hb_lane.hpp"
 
+// Set by hb_ctx_prepare on its thread: the launchers only load code objects
+// (hb_kernels.hpp, HB_LAUNCH).  Defined in hb_kern_misc.hip.
+extern thread_local bool hb_load_only;
+
 // Workgroup geometry of the PRF engine kernels: 1024 threads (16 waves) and a
 // 128 KiB LDS T-table image per workgroup -> 1 workgroup (16 waves) per CU.
 #ifndef HB_ENGINE_WG
@@ -163,12 +167,13 @@ struct WsumArgs {
     const u32 *vals;
     u32 *partials;                // [ncols][gridDim.x][NL]
     unsigned int *ctl;            // ncols + 1 counters, zero between launches
-    u32 *out;                     // [ncols][NL] results, then one status word
+    u32 *out;                     // [ncols][NL] results, the status word, the token word
     u32 accumulate;               // out[col] += this launch's sum
     u32 finalize;                 // record + zero the PRF slots and flags
     unsigned long long *qslots;   // nslots PRF engine slots (HB_QSLOT counters each)
     u32 nslots;
     unsigned int *flags;
+    u32 token;                    // this launch's completion token (never 0), see hb_wsum_kernel
 };
 
 // Merkle chunk positions and leaves (heartbeat/Merkle/Merkle.py:481-515),

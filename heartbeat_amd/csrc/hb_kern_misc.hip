@@ -3,6 +3,8 @@
 // challenge indices.
 #include "hb_kernels.hpp"
 
+thread_local bool hb_load_only = false;
+
 hipError_t hb_launch_prefix(const PrefixArgs &A, int nr, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);
     if (nr == 14) HB_LAUNCH((hb_prefix_kernel<14>), g, b, s, A);

@@ -1181,6 +1181,44 @@ __device__ __forceinline__ void hb_tree_sum(u32 *sh, u32 n) {
 // also records the PRF engines' abandoned-job counts and the index flags in
 // out[ncols*NL] and zeroes the counters for the next operation: a prove is
 // two launches with no memset.
+//
+// Cross-workgroup protocol and the invariants it rests on (a result is only
+// as good as these):
+//  I1  ctl[0 .. ncols] are 0 when a launch starts.  Established by the
+//      allocation memset (hb_runtime.cpp ensure_ctl) and re-established by
+//      every launch that runs to its end: each column's finisher stores
+//      ctl[col] = 0 after the column's last increment, the closer (the last
+//      column to finish) stores ctl[ncols] = 0; a prove cut short between
+//      its launches makes the host clear them (prove_dirty).  Every
+//      workgroup increments its column's counter exactly once (no path
+//      returns before the increment), so in a launch that starts with I1 the
+//      counter of every column reaches gridDim.x exactly once.
+//  I2  Partials are published before the counter (release) and read by the
+//      finisher after it (acquire), both at agent scope.
+//  I3  out[] is written only by column finishers and the closer, and read by
+//      the host (or an `accumulate` launch) only after the launch completed
+//      (stream order).
+//  I4  The PRF slots and the index flag word are read and cleared once per
+//      operation, by the closer of the finalizing launch, after every column
+//      is done (the PRF kernel that wrote them precedes in stream order).
+// If I1 fails, a column's finisher does not run (a stale count >= gridDim.x
+// means the column's counter never hits gridDim.x) or runs early, and out[col]
+// silently keeps what it held before -- the round-4 failure of an
+// experimental variant (profiles/r04/q/gpu_tests_wsa_early_status_only.log):
+// the first 2048-bit prove of the process, one workgroup per column, returned
+// a mu of an empty file that was not a sum at all but stale memory (words 0,
+// 16 and 24 = 0x7f / 0x9f / 0x7f, the layout of the engine-queue counters;
+// the same words in two runs with different histories), i.e. the column's
+// finisher had not written out[0 .. NL) in that launch.  (The variant's
+// source was not kept, so the write that broke I1 there is not named here;
+// the shipped kernel keeps I1 by the resets above.)
+// So the host no longer trusts a result the closer did not vouch for: every
+// launch's closer writes out[ncols*NL + 1] = token (distinct per launch,
+// never 0) -- an `accumulate` launch only if the word still holds the
+// previous launch's token (token - 1), else 0 -- and the host rejects the
+// result unless the word equals the last launch's token (finish_sums).  A
+// launch in which some column never finished, or a batch chain with a gap,
+// is thereby a loud error, not a wrong proof.
 template <int NL, int ALIGN>
 __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
     __shared__ u32 sh[HB_WSUM_WG * (NL + 1)];
@@ -1253,6 +1291,9 @@ __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
         const unsigned int d = __hip_atomic_fetch_add(A.ctl + A.ncols, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (d + 1 == A.ncols) {
             A.ctl[A.ncols] = 0;
+            // completion token (see above): every column of this launch is done
+            u32 *tok = A.out + (u64)A.ncols * NL + 1;
+            *tok = !A.accumulate || *tok == A.token - 1u ? A.token : 0u;
             if (A.finalize) {
                 u32 st = 0;
                 for (u32 s = 0; s < A.nslots; ++s) {
@@ -1273,18 +1314,21 @@ __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
 
 // ------------------------------------------------------------------ launchers
 // Plain C++ entry points for hb_runtime.cpp (explicit instantiation per
-// limb count NL, AES rounds NR and sector alignment class).  A grid of 0
-// launches nothing: it only makes the runtime load the kernel's code object
-// (hb_ctx_prepare), which otherwise happens inside the first launch.
+// limb count NL, AES rounds NR and sector alignment class).  While the
+// calling thread has hb_load_only set (hb_ctx_prepare, HbLoadOnly in
+// hb_runtime.cpp) a launcher launches nothing: it only makes the runtime load
+// the kernel's code object, which otherwise happens inside the first launch.
+// Otherwise a grid with a zero dimension is an error, never a silent no-op.
 template <class K>
 __host__ inline void hb_load_kernel(K *k) {
     hipFuncAttributes fa;
     (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(k));
 }
-#define HB_LAUNCH(KT, G, B, S, A)                          \
-    do {                                                   \
-        if ((G).x) hipLaunchKernelGGL(KT, G, B, 0, S, A);  \
-        else hb_load_kernel(&KT);                          \
+#define HB_LAUNCH(KT, G, B, S, A)                                          \
+    do {                                                                   \
+        if (hb_load_only) hb_load_kernel(&KT);                             \
+        else if (!(G).x || !(G).y) return hipErrorInvalidConfiguration;    \
+        else hipLaunchKernelGGL(KT, G, B, 0, S, A);                        \
     } while (0)
 // pass: 0 = single-pass engine, 1 = first tries (prefix image), 2 = retry list,
 // 3 = cxx prf encode

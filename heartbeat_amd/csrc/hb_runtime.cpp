@@ -13,6 +13,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -100,7 +103,13 @@ struct hb_ctx {
     // (not yet waited for: the next round trip must wait before reusing hscratch)
     hipEvent_t ev_alpha = nullptr, ev_h2d = nullptr;
     bool h2d_pending = false;
+    bool alpha_pending = false;   // the alpha D2H into hscratch not yet waited for
     bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
+    bool ctl_dirty = false;     // a weighted sum did not complete: clear its counters
+    u32 wsum_token = 0;         // completion token of the last hb_wsum_kernel launch
+    // HB_ENABLE_TEST_SWITCHES=1 when the context was created: the A/B and test
+    // switches (sw_env) are honoured; otherwise none is even read
+    bool switches = false;
     u32 *hres = nullptr; // pinned host copy of wsum results (+ status)
     size_t hres_n = 0;
     std::string err;
@@ -132,6 +141,40 @@ int hipfail(hb_ctx *c, hipError_t e, const char *what) {
         hipError_t e_ = (expr);                      \
         if (e_ != hipSuccess) return hipfail(c, e_, what); \
     } while (0)
+
+// ------------------------------------------------------------------ A/B and test switches
+// Environment switches that change HOW a result is computed (never what):
+// engine and MAC variants for same-box A/Bs, shrunken buffers that force the
+// overflow / multi-batch paths in tests, phase tracing.  All are behind one
+// gate, HB_ENABLE_TEST_SWITCHES=1, read once when a context is created, so a
+// stray variable in a production environment cannot change the speed.
+// (HB_GATHER_THREADS, a deployment knob, is not a test switch.)
+bool switch_gate() {
+    const char *g = getenv("HB_ENABLE_TEST_SWITCHES");
+    return g && g[0] == '1' && g[1] == 0;
+}
+
+const char *sw_env(const hb_ctx *c, const char *name) {
+    if (!c->switches) return nullptr;
+    const char *v = getenv(name);
+    return v && *v ? v : nullptr;
+}
+
+struct SwitchName {
+    const char *env;
+    u32 bit;
+};
+const SwitchName kSwitches[] = {
+    {"HB_NO_QUAD", HB_SW_NO_QUAD},
+    {"HB_NO_MFMA", HB_SW_NO_MFMA},
+    {"HB_MFMA_SECTOR_LOADS", HB_SW_MFMA_SECTOR_LOADS},
+    {"HB_MFMA_LINE32", HB_SW_MFMA_LINE32},
+    {"HB_MFMA_MIN_S", HB_SW_MFMA_MIN_S},
+    {"HB_TEST_NO_EARLY_LIST", HB_SW_NO_EARLY_LIST},
+    {"HB_TEST_RETRY_CAP", HB_SW_RETRY_CAP},
+    {"HB_TEST_PROVE_BATCH", HB_SW_PROVE_BATCH},
+    {"HB_TRACE_PHASES", HB_SW_TRACE_PHASES},
+};
 
 int nl_for_bits(int bits) {
     if (bits <= 64) return 2;
@@ -197,7 +240,7 @@ EngineShape small_engine(hb_ctx *c, u64 njobs) {
 // bound by their longest serial CFB chain, not by throughput.  Every CU, one
 // job per quad per refill (16 per wave).
 bool use_quad(hb_ctx *c, u64 njobs) {
-    if (getenv("HB_NO_QUAD")) return false;   // A/B and parity tests: the lane engine
+    if (sw_env(c, "HB_NO_QUAD")) return false;   // A/B and parity tests: the lane engine
     return njobs > 0 && 4 * njobs <= (u64)c->num_cus * HB_ENGINE_WG;
 }
 EngineShape quad_engine(hb_ctx *c, u64 njobs) {
@@ -292,8 +335,14 @@ bool full16(const PrimeInfo &pi, int nl, u64 C, const void *base) {
 // The HIP runtime loads a translation unit's code object (hb_kern_*.hip, up
 // to ~3 MiB each) at the first launch of one of its kernels.  hb_ctx_prepare
 // does that ahead of the first encode / prove with a prime of the given size:
-// every launcher is called with a grid of 0, which only loads the kernel
-// (hb_kernels.hpp, HB_LAUNCH).
+// every launcher is called with hb_load_only set on this thread, which only
+// loads the kernel (hb_kernels.hpp, HB_LAUNCH); the flag is cleared again on
+// every exit path, so no real launch can be skipped.
+struct HbLoadOnly {
+    HbLoadOnly() { hb_load_only = true; }
+    ~HbLoadOnly() { hb_load_only = false; }
+};
+
 template <int NL>
 void prepare_nl(hb_ctx *c) {
     EncodeArgs<NL> E;
@@ -320,7 +369,7 @@ void prepare_nl(hb_ctx *c) {
 // block with probability q = 1 - p / 2^bitlen(p); room for the mean plus 8
 // standard deviations (a block that finds the list full is finished in place
 // by the first-pass kernel, so the bound only affects speed, never results).
-u64 retry_capacity(const uint8_t *p_be, size_t p_len, u64 nb) {
+u64 retry_capacity(const hb_ctx *c, const uint8_t *p_be, size_t p_len, u64 nb) {
     size_t i = 0;
     while (i < p_len && p_be[i] == 0) ++i;
     u64 top = 0;
@@ -333,7 +382,7 @@ u64 retry_capacity(const uint8_t *p_be, size_t p_len, u64 nb) {
     const double mean = q * (double)nb;
     double cap = mean + 8.0 * sqrt(mean) + 1024.0;
     // test hook: a smaller list, to exercise the in-place overflow path
-    if (const char *t = getenv("HB_TEST_RETRY_CAP")) cap = fmin(cap, atof(t));
+    if (const char *t = sw_env(c, "HB_TEST_RETRY_CAP")) cap = fmin(cap, atof(t));
     return cap >= (double)nb ? nb : (u64)cap;
 }
 
@@ -372,6 +421,12 @@ int mfma_tables_begin(hb_ctx *c, u32 S) {
         HB_CHECK(hipEventSynchronize(c->ev_h2d), "H2D(afrag)");
         c->h2d_pending = false;
     }
+    if (c->alpha_pending) {
+        // an encode that failed between its alpha D2H and mfma_tables: that
+        // copy may still be writing hscratch (error path only)
+        HB_CHECK(hipStreamSynchronize(c->stream), "D2H(alpha)");
+        c->alpha_pending = false;
+    }
     HB_CHECK(c->hscratch.ensure((size_t)S * NL * 4 + (size_t)HB_MFMA_NT * S * 64 * 16), "hipHostMalloc(scratch)");
 #if !defined(HB_MFMA_TOEPLITZ) && !defined(HB_MAC_MONT)
     // the dense tiles carry alpha_j itself (the finish adds F and reduces,
@@ -381,6 +436,7 @@ int mfma_tables_begin(hb_ctx *c, u32 S) {
     const void *asrc = c->alpha_mont.p;
 #endif
     HB_CHECK(hipMemcpyAsync(c->hscratch.p, asrc, (size_t)S * NL * 4, hipMemcpyDeviceToHost, c->stream), "D2H(alpha)");
+    c->alpha_pending = true;   // until mfma_tables (or the next begin) waits for ev_alpha
     HB_CHECK(hipEventRecord(c->ev_alpha, c->stream), "hipEventRecord");
     return 0;
 }
@@ -391,6 +447,7 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
     int8_t *frag = (int8_t *)c->hscratch.p + (size_t)S * NL * 4;
     const size_t frag_bytes = (size_t)HB_MFMA_NT * S * 64 * 16;
     HB_CHECK(hipEventSynchronize(c->ev_alpha), "alpha PRF");
+    c->alpha_pending = false;
     // layouts 1, 2 (32x32x32 B operand): slot s, lane half h, byte e ->
     // (sector j, byte k of sector j)
     auto src_of = [&](u32 slot, int h, int e, u32 &j, int &k) {
@@ -577,6 +634,143 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
     return 0;
 }
 
+// HB_HOST_REGISTER: the host bytes [data, data + len) page-locked read-only
+// (hipHostRegisterReadOnly: a PROT_READ file mapping cannot be registered for
+// writing) in page-aligned windows of kWindow bytes.  A helper thread
+// registers up to kAhead windows ahead of the chunk being copied -- the page
+// pinning overlaps the DMA of the previous window -- and unregisters each
+// window once the copy-stream event recorded after its last chunk has
+// completed, so at most about kAhead + 2 windows are pinned at a time.  A
+// window whose registration fails (e.g. memory the caller registered
+// already) is simply copied unpinned.  The reference reads the file through
+// Python read() calls (PySwizzle.py:299; cxx/PythonSeekableFile.hxx:47-54);
+// this is the replacement's staging.
+struct HostWindows {
+    static constexpr u64 kWindow = 256ull << 20;
+    static constexpr u64 kAhead = 2;
+    enum { NONE = 0, PINNED, UNPINNED, RECORDED, DONE };
+    hb_ctx *c;
+    uintptr_t base = 0, end = 0;
+    u64 nwin = 0;
+    std::vector<int> state;
+    std::vector<hipEvent_t> ev;
+    std::mutex m;
+    std::condition_variable cv;
+    u64 allowed = 0;        // windows [0, allowed) may be registered
+    u64 next_reg = 0;       // next window the helper registers
+    u64 next_rec = 0;       // next window the main thread records an event for
+    bool quit = false;
+    std::thread th;
+
+    HostWindows(hb_ctx *ctx, const uint8_t *data, u64 len) : c(ctx) {
+        base = (uintptr_t)data & ~(uintptr_t)4095;
+        end = ((uintptr_t)data + len + 4095) & ~(uintptr_t)4095;
+        nwin = len ? (end - base + kWindow - 1) / kWindow : 0;
+        state.assign((size_t)nwin, NONE);
+        ev.assign((size_t)nwin, nullptr);
+        th = std::thread([this] { run(); });
+    }
+    ~HostWindows() { finish(); }
+    u64 window_of(uintptr_t a) const { return (u64)((a - base) / kWindow); }
+    uintptr_t wlo(u64 w) const { return base + w * kWindow; }
+    uintptr_t whi(u64 w) const { return base + (w + 1) * kWindow < end ? base + (w + 1) * kWindow : end; }
+
+    void run() {
+        (void)hipSetDevice(c->device);
+        std::unique_lock<std::mutex> lk(m);
+        for (;;) {
+            if (next_reg < nwin && next_reg < allowed && !quit) {
+                const u64 w = next_reg;
+                lk.unlock();
+                const hipError_t e = hipHostRegister((void *)wlo(w), (size_t)(whi(w) - wlo(w)), hipHostRegisterReadOnly);
+                if (e != hipSuccess) (void)hipGetLastError();
+                lk.lock();
+                state[(size_t)w] = e == hipSuccess ? (int)PINNED : (int)UNPINNED;
+                ++next_reg;
+                cv.notify_all();
+                continue;
+            }
+            // a window whose last copy is enqueued: unpin it once that copy is done
+            u64 u = nwin;
+            for (u64 k = 0; k < nwin; ++k)
+                if (state[(size_t)k] == RECORDED) { u = k; break; }
+            if (u < nwin) {
+                lk.unlock();
+                (void)hipEventSynchronize(ev[(size_t)u]);
+                (void)hipHostUnregister((void *)wlo(u));
+                lk.lock();
+                state[(size_t)u] = DONE;
+                cv.notify_all();
+                continue;
+            }
+            if (quit) return;
+            cv.wait(lk);
+        }
+    }
+    // before copying [a, b): allow registration through the window of b plus
+    // kAhead more, and wait until the windows of [a, b) are settled
+    void acquire(uintptr_t a, uintptr_t b) {
+        const u64 wb = window_of(b - 1);
+        std::unique_lock<std::mutex> lk(m);
+        if (wb + 1 + kAhead > allowed) {
+            allowed = wb + 1 + kAhead;
+            cv.notify_all();
+        }
+        cv.wait(lk, [&] { return next_reg > wb; });
+        (void)a;
+    }
+    // every window below the one holding address a is copied for good: record
+    // an event on the copy stream behind those copies, for the helper
+    int release_below(uintptr_t a) {
+        const u64 wa = a >= end ? nwin : window_of(a);
+        while (next_rec < wa) {
+            const u64 w = next_rec++;
+            std::unique_lock<std::mutex> lk(m);
+            if (state[(size_t)w] != PINNED) {
+                if (state[(size_t)w] == UNPINNED) state[(size_t)w] = DONE;
+                continue;
+            }
+            lk.unlock();
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(e, c->copy) != hipSuccess) {
+                if (e) (void)hipEventDestroy(e);
+                (void)hipStreamSynchronize(c->copy);
+                e = nullptr;
+            }
+            lk.lock();
+            ev[(size_t)w] = e;
+            if (e) state[(size_t)w] = RECORDED;
+            else {
+                (void)hipHostUnregister((void *)wlo(w));
+                state[(size_t)w] = DONE;
+            }
+            cv.notify_all();
+        }
+        return 0;
+    }
+    // stop the helper; every window still pinned is unpinned after the copy
+    // stream has drained (all exit paths, errors included)
+    void finish() {
+        if (!th.joinable()) return;
+        {
+            std::lock_guard<std::mutex> lk(m);
+            quit = true;
+            cv.notify_all();
+        }
+        th.join();
+        bool any = false;
+        for (u64 w = 0; w < nwin; ++w) any = any || state[(size_t)w] == PINNED || state[(size_t)w] == RECORDED;
+        if (any) (void)hipStreamSynchronize(c->copy);
+        for (u64 w = 0; w < nwin; ++w) {
+            if (state[(size_t)w] == PINNED || state[(size_t)w] == RECORDED) (void)hipHostUnregister((void *)wlo(w));
+            if (ev[(size_t)w]) (void)hipEventDestroy(ev[(size_t)w]);
+            ev[(size_t)w] = nullptr;
+            state[(size_t)w] = DONE;
+        }
+    }
+};
+
 // Complete an HB_ASYNC encode: wait for its kernels, read its PRF counters;
 // the status is kept for hb_ctx_wait.  Every other entry point settles first
 // (its own kernels would reuse the counters and scratch buffers).
@@ -614,7 +808,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     const u64 C = (u64)pi.ss * S;
     // $HB_TRACE_PHASES: host-side phase times of this call on stderr (the
     // stream is synchronized at each mark; diagnosis of first-call costs)
-    static const bool trace = getenv("HB_TRACE_PHASES") != nullptr;
+    const bool trace = sw_env(c, "HB_TRACE_PHASES") != nullptr;
     const auto t_start = std::chrono::steady_clock::now();
     auto mark = [&](const char *what) {
         if (!trace) return;
@@ -645,10 +839,12 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         // (below 4 sectors per block the VALU MAC is cheaper than the MFMA
         // phase's fixed cost: at configs[1], S = 1, the m16 MFMA MAC measured
         // 70.98 vs 71.32 GiB/s, same-box A/B, profiles/r04/l)
-        // $HB_MFMA_MIN_S: the smallest sector count given the MFMA MAC (A/B)
-        static const u32 min_s = getenv("HB_MFMA_MIN_S") ? (u32)atoi(getenv("HB_MFMA_MIN_S")) : 4u;
+        // $HB_MFMA_MIN_S: the smallest sector count given the MFMA MAC (A/B,
+        // read per call like every switch)
+        const char *ms = sw_env(c, "HB_MFMA_MIN_S");
+        const u32 min_s = ms ? (u32)atoi(ms) : 4u;
         if (!cxx && pi.ss == 32 && S >= min_s && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
-            !getenv("HB_NO_MFMA")) {
+            !sw_env(c, "HB_NO_MFMA")) {
             // 3: the 16x16x64 MFMA, whose B operand is the whole-line load
             // shape (S even); 2: 32x32x32 with whole-line loads and an
             // in-quad transpose (S % 4 == 0; $HB_MFMA_LINE32, A/B); 1:
@@ -656,17 +852,15 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 #if defined(HB_NO_LINE_LOADS)
             const int layout = 1;
 #else
-            const bool sector = getenv("HB_MFMA_SECTOR_LOADS") != nullptr;
+            const bool sector = sw_env(c, "HB_MFMA_SECTOR_LOADS") != nullptr;
 #if defined(HB_MFMA_TOEPLITZ)
             const bool m16 = false;
 #else
-            const bool m16 = S % 2 == 0 && !sector && !getenv("HB_MFMA_LINE32");
+            const bool m16 = S % 2 == 0 && !sector && !sw_env(c, "HB_MFMA_LINE32");
 #endif
             const int layout = m16 ? 3 : S % 4 == 0 && !sector ? 2 : 1;
 #endif
-            rc = mfma_tables_begin(c, S);
-            if (rc) return rc;
-            mf_layout = layout;
+            mf_layout = layout;   // tables: mfma_tables_begin / mfma_tables below
         }
     }
     int nr = 0;
@@ -675,7 +869,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     if (A.prf.nb >= 4) A.rtop = hb_range_top<NL>(A.prf);
     // test hook: no early retry listing (every rejected first try is listed
     // after the try without its digest, and the retry pass hashes the index)
-    if (getenv("HB_TEST_NO_EARLY_LIST")) A.rtop = 0xffffffffu;
+    if (sw_env(c, "HB_TEST_NO_EARLY_LIST")) A.rtop = 0xffffffffu;
     A.alpha_mont = (const u32 *)c->alpha_mont.p;
     A.t0 = c->t0;
     A.C = C;
@@ -703,7 +897,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // (profiles/r02/s8)
     const bool two_pass = !cxx && A.prf.nb >= 4 && !(flags & HB_ENCODE_SINGLE_PASS);
     if (two_pass) {
-        A.retry_cap = retry_capacity(p_be, p_len, launch_blocks);
+        A.retry_cap = retry_capacity(c, p_be, p_len, launch_blocks);
         HB_CHECK(c->retry.ensure((size_t)(A.retry_cap ? A.retry_cap : 1) * sizeof(HbRetry)), "hipMalloc(retry)");
         A.retry = (HbRetry *)c->retry.p;
         A.retry_count = q0 + 3;
@@ -718,6 +912,12 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         aes_encrypt_block(k, zero, o);
         A.o0 = o[0];
         mark("prefix image buffer");
+    }
+    if (mf_layout) {
+        // every argument check and allocation is behind us: the alpha D2H
+        // into hscratch starts here (mfma_tables waits for it)
+        rc = mfma_tables_begin(c, S);
+        if (rc) return rc;
     }
     c->last_launches = 0;
     float ms_total = 0.f;
@@ -789,6 +989,8 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         // chunk on the compute stream.
         HB_CHECK(c->data[0].ensure((size_t)(cb * C)), "hipMalloc(staging)");
         HB_CHECK(c->data[1].ensure((size_t)(cb * C)), "hipMalloc(staging)");
+        std::unique_ptr<HostWindows> hw;
+        if ((flags & HB_HOST_REGISTER) && len) hw.reset(new HostWindows(c, data, len));
         auto tags_back = [&](u64 k, u64 n, int buf) -> int {
             HB_CHECK(hipStreamWaitEvent(c->copy, c->done[buf], 0), "hipStreamWaitEvent");
             HB_CHECK(hipMemcpyAsync(tags + k * pi.tw, dtags + k * pi.tw, (size_t)(n * pi.tw),
@@ -804,9 +1006,22 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             const u64 end = (k0 + nb) * C < len ? (k0 + nb) * C : len;
             const u64 bytes = end > off ? end - off : 0;
             if (it >= 2) HB_CHECK(hipStreamWaitEvent(c->copy, c->done[b], 0), "hipStreamWaitEvent");
-            if (bytes)
+            if (bytes && hw) {
+                // pinned windows: one DMA per window piece of the chunk
+                const uintptr_t a = (uintptr_t)(data + off), e = (uintptr_t)(data + end);
+                hw->acquire(a, e);
+                for (uintptr_t x = a; x < e;) {
+                    const uintptr_t y = hw->whi(hw->window_of(x)) < e ? hw->whi(hw->window_of(x)) : e;
+                    HB_CHECK(hipMemcpyAsync((uint8_t *)c->data[b].p + (x - a), (const void *)x, (size_t)(y - x),
+                                            hipMemcpyHostToDevice, c->copy),
+                             "hipMemcpyAsync(H2D)");
+                    x = y;
+                }
+                hw->release_below(e);
+            } else if (bytes) {
                 HB_CHECK(hipMemcpyAsync(c->data[b].p, data + off, (size_t)bytes, hipMemcpyHostToDevice, c->copy),
                          "hipMemcpyAsync(H2D)");
+            }
             HB_CHECK(hipEventRecord(c->copied[b], c->copy), "hipEventRecord");
             HB_CHECK(hipStreamWaitEvent(c->stream, c->copied[b], 0), "hipStreamWaitEvent");
             rc = launch((const uint8_t *)c->data[b].p, bytes, nb, block_base + k0, dtags + k0 * pi.tw);
@@ -828,6 +1043,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
         HB_CHECK(hipEventSynchronize(c->k1), "encode");
         HB_CHECK(hipEventElapsedTime(&ms_total, c->k0, c->k1), "hipEventElapsedTime");
+        if (hw) hw->finish();
     }
     c->last_ms = ms_total;
     if (!tags_dev && data_dev)
@@ -876,28 +1092,51 @@ u32 wsum_grid(u64 nterms) {
 }
 
 // Launch a weighted-sum pass with results in c->sums (ncols * NL + status).
+// Completion tokens of hb_wsum_kernel launches: consecutive within an
+// operation (an `accumulate` launch checks for its predecessor's, token - 1),
+// never 0; restarted well before the counter would wrap.
+u32 next_token(hb_ctx *c, bool first_of_operation) {
+    if (first_of_operation && c->wsum_token > 0xfff00000u) c->wsum_token = 0;
+    return ++c->wsum_token;
+}
+
 template <int NL>
 int launch_wsum(hb_ctx *c, WsumArgs<NL> &A, int align) {
     const u32 gx = wsum_grid(A.nterms);
     HB_CHECK(c->partials.ensure((size_t)A.ncols * gx * NL * 4), "hipMalloc(partials)");
-    HB_CHECK(c->sums.ensure(((size_t)A.ncols * NL + 1) * 4), "hipMalloc(sums)");
+    HB_CHECK(c->sums.ensure(((size_t)A.ncols * NL + 2) * 4), "hipMalloc(sums)");
     if (int rc = ensure_ctl(c, A.ncols)) return rc;
+    if (c->ctl_dirty) {
+        // an earlier weighted sum did not complete (finish_sums): its column
+        // counters may be left non-zero (hb_wsum_kernel, invariant I1)
+        HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync(ctl)");
+        c->ctl_dirty = false;
+    }
     A.partials = (u32 *)c->partials.p;
     A.ctl = (unsigned int *)c->ctl.p;
     A.flags = flags_word(c);
     A.out = (u32 *)c->sums.p;
+    A.token = next_token(c, !A.accumulate);
     HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");
     return 0;
 }
 
 // After the finalizing wsum: copy the results back (one D2H), check the
-// status word, write the ncols values big-endian (tw bytes each) to out.
+// completion token and the status word, write the ncols values big-endian
+// (tw bytes each) to out.
 template <int NL>
 int finish_sums(hb_ctx *c, u32 ncols, u32 tw, uint8_t *out, bool cxx_index_check) {
-    const size_t words = (size_t)ncols * NL + 1;
+    const size_t words = (size_t)ncols * NL + 2;
     if (int rc = ensure_hres(c, words)) return rc;
     HB_CHECK(hipMemcpyAsync(c->hres, c->sums.p, words * 4, hipMemcpyDeviceToHost, c->stream), "hipMemcpy");
     HB_CHECK(hipStreamSynchronize(c->stream), "prove");
+    if (c->hres[(size_t)ncols * NL + 1] != c->wsum_token) {
+        // some column's finisher (or a batch) did not run: out[] is not this
+        // operation's result (hb_wsum_kernel, I1).  Loud, and the counters are
+        // cleared before the next weighted sum.
+        c->ctl_dirty = true;
+        return fail(c, HB_EHIP, "internal: weighted sum did not complete (completion token mismatch)");
+    }
     const u32 st = c->hres[(size_t)ncols * NL];
     if (st & 2u) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate");
     if ((st & 1u) && cxx_index_check)
@@ -997,6 +1236,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
                  "hipMemsetAsync");
         if (c->ctl.n) HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync");
         c->prove_dirty = false;
+        c->ctl_dirty = false;
     }
     // stage 1: idx_i = KeyedPRF(key, ntags)(i), v_i = KeyedPRF(key, v_max)(i)   (PySwizzle.py:344-345)
     ProveArgs<NL> PA;
@@ -1103,7 +1343,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         // of page-locked host memory per context until hb_ctx_destroy)
         u64 per = (u64)((64ull << 20) / (C + pi.tw)) ? (64ull << 20) / (C + pi.tw) : 1;
         // test hook: smaller batches, to exercise the double buffering
-        if (const char *t = getenv("HB_TEST_PROVE_BATCH")) {
+        if (const char *t = sw_env(c, "HB_TEST_PROVE_BATCH")) {
             const u64 cap = (u64)strtoull(t, nullptr, 10);
             if (cap >= 1 && cap < per) per = cap;
         }
@@ -1144,7 +1384,9 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
     std::vector<uint8_t> out((size_t)ncols * pi.tw);
     rc = finish_sums<NL>(c, ncols, pi.tw, out.data(), cxx && !check_all);
-    c->prove_dirty = false;   // the finalizing launch ran (its status decides rc)
+    // the finalizing launch ran to its end (its status decides rc) unless the
+    // completion token says otherwise: then its PRF slots were not cleared
+    c->prove_dirty = c->ctl_dirty;
     if (rc) return rc;
     float ms = 0.f;
     HB_CHECK(hipEventElapsedTime(&ms, c->k0, c->k1), "hipEventElapsedTime");
@@ -1230,10 +1472,22 @@ int hb_abi_version(void) { return HB_ABI_VERSION; }
 
 int hb_build_flags(void) {
 #if defined(HB_EXPERIMENT_BUILD)
-    return HB_BUILD_EXPERIMENT;
+    int f = HB_BUILD_EXPERIMENT;
 #else
-    return 0;
+    int f = 0;
 #endif
+    if (switch_gate()) f |= HB_BUILD_TEST_SWITCHES;
+    return f;
+}
+
+uint32_t hb_test_switches(void) {
+    if (!switch_gate()) return 0;
+    u32 m = 0;
+    for (const SwitchName &s : kSwitches) {
+        const char *v = getenv(s.env);
+        if (v && *v) m |= s.bit;
+    }
+    return m;
 }
 
 int hb_device_count(int *n) {
@@ -1267,6 +1521,7 @@ int hb_ctx_create(int device, hb_ctx **out) {
     }
     hb_ctx *c = new hb_ctx();
     c->device = device;
+    c->switches = switch_gate();   // the test-switch gate, read once per context
     auto bad = [&](hipError_t err, const char *what) {
         g_create_error = std::string(what) + ": " + hipGetErrorString(err);
         hb_ctx_destroy(c);
@@ -1350,6 +1605,7 @@ int hb_ctx_prepare(hb_ctx *c, uint32_t prime_bits) {
     int nl = nl_for_bits((int)prime_bits);
     if (!nl) return fail(c, HB_EUNSUPPORTED, "primes above 2048 bits are not supported by this build");
     if (nl < 8) nl = 8;
+    HbLoadOnly load_only;
     PrefixArgs PA;
     memset(&PA, 0, sizeof PA);
     (void)hb_launch_prefix(PA, 14, 0, c->stream);

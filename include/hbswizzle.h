@@ -58,6 +58,18 @@ extern "C" {
                         caller's stream ("an async variant takes a
                         hipStream_t"). */
 
+#define HB_HOST_REGISTER 32u  /* hb_encode with host data: page-lock the file bytes
+                                 read-only (hipHostRegisterReadOnly) in windows of
+                                 256 MiB, one window ahead of the copy on a helper
+                                 thread, and DMA the chunks straight from them
+                                 (unregistered once copied), instead of the
+                                 runtime's pageable staging.  For read-only
+                                 mappings of files (the reference's file object,
+                                 PySwizzle.py:299) and other large host buffers;
+                                 a window that cannot be registered (e.g. already
+                                 registered by the caller) is copied as is.  Same
+                                 tags. */
+
 /* error codes */
 #define HB_OK 0
 #define HB_EINVAL -1
@@ -71,9 +83,35 @@ int hb_abi_version(void);
 
 /* Build properties.  HB_BUILD_EXPERIMENT: an A/B experiment build
  * (scripts/build_variant.sh) whose HB_EXP_* switches may emit wrong tags; the
- * Python package refuses such a library unless HB_LIB_PATH names it. */
+ * Python package refuses such a library unless HB_LIB_PATH names it.
+ * HB_BUILD_TEST_SWITCHES: HB_ENABLE_TEST_SWITCHES=1 is set in this process's
+ * environment, so contexts created now honour the A/B and test switches
+ * (hb_test_switches) -- never set for measurements. */
 #define HB_BUILD_EXPERIMENT 1
+#define HB_BUILD_TEST_SWITCHES 2
 int hb_build_flags(void);
+
+/* Provenance: hex SHA-256 of every source file of this library
+ * (heartbeat_amd/csrc, this header) and of its compiler flags, as computed by
+ * heartbeat_amd/build_id.py at build time; and those flags.  The Python
+ * package refuses a library whose id does not match the tree it sits in. */
+const char *hb_build_id(void);
+const char *hb_build_flags_string(void);
+
+/* The A/B and test switches (environment variables) a
+ * context created now would honour, as a bit mask (HB_SW_*).  All of them
+ * are ignored -- mask 0 -- unless HB_ENABLE_TEST_SWITCHES=1 is set when the
+ * context is created; a context reads that gate once, at creation. */
+#define HB_SW_NO_QUAD 1u
+#define HB_SW_NO_MFMA 2u
+#define HB_SW_MFMA_SECTOR_LOADS 4u
+#define HB_SW_MFMA_LINE32 8u
+#define HB_SW_MFMA_MIN_S 16u
+#define HB_SW_NO_EARLY_LIST 32u
+#define HB_SW_RETRY_CAP 64u
+#define HB_SW_PROVE_BATCH 128u
+#define HB_SW_TRACE_PHASES 256u
+uint32_t hb_test_switches(void);
 
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens
  * one context per device; contexts fail on non-gfx950 devices). */

@@ -10,6 +10,14 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# The GPU tests that select engine / MAC variants or shrink buffers through
+# environment switches (HB_NO_QUAD, HB_MFMA_*, HB_TEST_*) need the gate open
+# when their context is created: libhbswizzle reads HB_ENABLE_TEST_SWITCHES
+# once per context and ignores every switch without it (hb_runtime.cpp).
+# Opened for the test session only; bench.py and smoke() never set it.  The
+# CPU test of the gate (test_provenance.py) closes it itself.
+os.environ["HB_ENABLE_TEST_SWITCHES"] = "1"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")

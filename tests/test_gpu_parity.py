@@ -308,6 +308,39 @@ def test_mfma_mac_sector_counts_vs_oracle(nat, oracle, S, prime_name):
         tb.free()
 
 
+@pytest.mark.parametrize("switch,S", [("HB_MFMA_LINE32", 20), ("HB_MFMA_LINE32", 36),
+                                      ("HB_MFMA_SECTOR_LOADS", 4), ("HB_MFMA_SECTOR_LOADS", 20)])
+def test_mfma_selectable_layouts_vs_oracle(nat, oracle, monkeypatch, switch, S):
+    """The MAC layouts the shipped build can still select by switch (ADVICE
+    r4): HB_MFMA_LINE32 -- the 32x32x32 MFMA with whole-line loads and the
+    in-quad DPP transpose (mfma_tables layout 2, S % 4 == 0) -- and
+    HB_MFMA_SECTOR_LOADS -- the 32x32x32 MFMA with sector-shaped loads (layout
+    1, here at even S, which the default build gives the 16x16x64 MAC).
+    Primes just below 2^256 (digit representatives at the edge of their range)
+    and p256; a ragged 2 MiB device-resident file; every tag == the oracle."""
+    primes = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))
+    monkeypatch.setenv(switch, "1")
+    L = (2 << 20) + 333
+    C = 32 * S
+    nb = L // C + 1
+    buf = DevBuf(nat, L)
+    tb = DevBuf(nat, nb * 32)
+    try:
+        ctx = nat.context()
+        assert nat.lib().hb_test_switches() != 0, "the test-switch gate is closed (tests/conftest.py)"
+        ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 2000 + S))
+        data = buf.download()
+        for prime_name in ("p256max", "p256"):
+            p = int(primes[prime_name], 16)
+            fk, ak = hashlib.sha256(b"lay-f%d" % S).digest(), hashlib.sha256(b"lay-a" + switch.encode()).digest()
+            dev_encode(nat, p, S, fk, ak, buf.p, L, nb, tb.p, block_base=77777)
+            want = oracle.encode(p, S, fk, ak, data, block_base=77777, nthreads=16)
+            assert split_tags(tb.download(), 32) == want, prime_name
+    finally:
+        buf.free()
+        tb.free()
+
+
 @pytest.mark.parametrize("S,prime_name", [(16, "p256"), (1, "p256"), (5, "p255"), (16, "p256lo"),
                                           (3, "p1024"), (4, "p61")])
 def test_two_pass_equals_single_pass(nat, S, prime_name):
