@@ -363,9 +363,12 @@ class PySwizzle(object):
 
 # Host buffers whose bytes hb_encode page-locks read-only in windows
 # (HB_HOST_REGISTER) instead of staging them through the runtime's pageable
-# copies, by FileBuffer kind; bench.py's host_path measures both ways
-# (DESIGN.md 6).
-REGISTER_KINDS = ()
+# copies, by FileBuffer kind.  Real files (read-only mmaps): a 4 GiB file
+# through encode_file measured 42.8 vs 31.7 GiB/s median of 5 on one box
+# (profiles/r05/c/probe6.json, caller-pinned raw rate 49.0); a BytesIO's
+# buffer did not gain (12.5 vs 16.7 in the same run), so it stays pageable.
+# bench.py's host_path measures both ways in every default run.
+REGISTER_KINDS = ("mmap",)
 
 
 def encode_file(p, sectors, f_key, alpha_key, file, devices=None, register=None):
@@ -380,7 +383,7 @@ def encode_file(p, sectors, f_key, alpha_key, file, devices=None, register=None)
     fk, ak = _kb(f_key), _kb(alpha_key)
     if len(fk) != len(ak):
         raise HeartbeatError("f_key and alpha_key must have the same length")
-    fb = FileBuffer(file)
+    fb = FileBuffer(file, populate=not register if register is not None else "mmap" not in REGISTER_KINDS)
     try:
         nblocks = fb.len // C + 1
         # the tags land in the array the Tag keeps: no zero fill, no copy of

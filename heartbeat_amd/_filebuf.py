@@ -40,7 +40,7 @@ import numpy as np
 
 
 class FileBuffer(object):
-    def __init__(self, file, from_start=False):
+    def __init__(self, file, from_start=False, populate=True):
         self._mm = None
         self.file = file
         self.from_start = from_start
@@ -74,10 +74,12 @@ class FileBuffer(object):
                     if size > start:
                         # encode reads every byte: prefault the mapping
                         # (MAP_POPULATE) instead of taking page faults inside
-                        # the staging copies; prove reads only the challenged
-                        # blocks and maps lazily
+                        # the staging copies -- unless the encode page-locks
+                        # the bytes itself (populate=False: the registration
+                        # faults them in, overlapped with the copies); prove
+                        # reads only the challenged blocks and maps lazily
                         flags = mmap.MAP_SHARED
-                        if not from_start and hasattr(mmap, "MAP_POPULATE"):
+                        if not from_start and populate and hasattr(mmap, "MAP_POPULATE"):
                             flags |= mmap.MAP_POPULATE
                         self._mm = mmap.mmap(fd, 0, flags=flags, prot=mmap.PROT_READ)
                         arr = np.frombuffer(self._mm, dtype=np.uint8)[start:]

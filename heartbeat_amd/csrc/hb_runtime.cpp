@@ -174,6 +174,8 @@ const SwitchName kSwitches[] = {
     {"HB_TEST_RETRY_CAP", HB_SW_RETRY_CAP},
     {"HB_TEST_PROVE_BATCH", HB_SW_PROVE_BATCH},
     {"HB_TRACE_PHASES", HB_SW_TRACE_PHASES},
+    {"HB_HOST_WINDOW_MIB", HB_SW_HOST_WINDOWS},
+    {"HB_HOST_AHEAD", HB_SW_HOST_WINDOWS},
 };
 
 int nl_for_bits(int bits) {
@@ -646,8 +648,8 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
 // Python read() calls (PySwizzle.py:299; cxx/PythonSeekableFile.hxx:47-54);
 // this is the replacement's staging.
 struct HostWindows {
-    static constexpr u64 kWindow = 256ull << 20;
-    static constexpr u64 kAhead = 2;
+    u64 kWindow = 256ull << 20;   // $HB_HOST_WINDOW_MIB (test switch, A/B)
+    u64 kAhead = 2;               // $HB_HOST_AHEAD (test switch, A/B)
     enum { NONE = 0, PINNED, UNPINNED, RECORDED, DONE };
     hb_ctx *c;
     uintptr_t base = 0, end = 0;
@@ -662,12 +664,23 @@ struct HostWindows {
     bool quit = false;
     std::thread th;
 
-    HostWindows(hb_ctx *ctx, const uint8_t *data, u64 len) : c(ctx) {
-        base = (uintptr_t)data & ~(uintptr_t)4095;
-        end = ((uintptr_t)data + len + 4095) & ~(uintptr_t)4095;
+    unsigned int reg_flags;
+    // host bytes [p, p + len); read_only: the device only reads them (the
+    // file), else it writes them (the tags); scale: window size relative to
+    // the file's (the tags of a file window: tw / C of it, so that the first
+    // tag copy waits for a small window only)
+    HostWindows(hb_ctx *ctx, const void *p, u64 len, bool read_only, double scale = 1.0)
+        : c(ctx), reg_flags(read_only ? hipHostRegisterReadOnly : hipHostRegisterDefault) {
+        if (const char *v = sw_env(c, "HB_HOST_WINDOW_MIB")) kWindow = (u64)(atoi(v) > 0 ? atoi(v) : 256) << 20;
+        if (const char *v = sw_env(c, "HB_HOST_AHEAD")) kAhead = (u64)(atoi(v) > 0 ? atoi(v) : 2);
+        kWindow = ((u64)((double)kWindow * scale) + 4095) & ~(u64)4095;
+        if (kWindow < (2ull << 20)) kWindow = 2ull << 20;
+        base = (uintptr_t)p & ~(uintptr_t)4095;
+        end = ((uintptr_t)p + len + 4095) & ~(uintptr_t)4095;
         nwin = len ? (end - base + kWindow - 1) / kWindow : 0;
         state.assign((size_t)nwin, NONE);
         ev.assign((size_t)nwin, nullptr);
+        allowed = kAhead + 1;   // start pinning right away, ahead of the first copy
         th = std::thread([this] { run(); });
     }
     ~HostWindows() { finish(); }
@@ -682,7 +695,7 @@ struct HostWindows {
             if (next_reg < nwin && next_reg < allowed && !quit) {
                 const u64 w = next_reg;
                 lk.unlock();
-                const hipError_t e = hipHostRegister((void *)wlo(w), (size_t)(whi(w) - wlo(w)), hipHostRegisterReadOnly);
+                const hipError_t e = hipHostRegister((void *)wlo(w), (size_t)(whi(w) - wlo(w)), reg_flags);
                 if (e != hipSuccess) (void)hipGetLastError();
                 lk.lock();
                 state[(size_t)w] = e == hipSuccess ? (int)PINNED : (int)UNPINNED;
@@ -989,13 +1002,29 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         // chunk on the compute stream.
         HB_CHECK(c->data[0].ensure((size_t)(cb * C)), "hipMalloc(staging)");
         HB_CHECK(c->data[1].ensure((size_t)(cb * C)), "hipMalloc(staging)");
-        std::unique_ptr<HostWindows> hw;
-        if ((flags & HB_HOST_REGISTER) && len) hw.reset(new HostWindows(c, data, len));
+        std::unique_ptr<HostWindows> hw, tw;
+        if ((flags & HB_HOST_REGISTER) && len) hw.reset(new HostWindows(c, data, len, true));
+        if ((flags & HB_HOST_REGISTER) && !tags_dev)
+            tw.reset(new HostWindows(c, tags, nblocks * pi.tw, false, (double)pi.tw / (double)C));
         auto tags_back = [&](u64 k, u64 n, int buf) -> int {
             HB_CHECK(hipStreamWaitEvent(c->copy, c->done[buf], 0), "hipStreamWaitEvent");
-            HB_CHECK(hipMemcpyAsync(tags + k * pi.tw, dtags + k * pi.tw, (size_t)(n * pi.tw),
-                                    hipMemcpyDeviceToHost, c->copy),
-                     "hipMemcpyAsync(D2H tags)");
+            if (!tw) {
+                HB_CHECK(hipMemcpyAsync(tags + k * pi.tw, dtags + k * pi.tw, (size_t)(n * pi.tw),
+                                        hipMemcpyDeviceToHost, c->copy),
+                         "hipMemcpyAsync(D2H tags)");
+                return 0;
+            }
+            // pinned tag windows: one DMA per window piece
+            const uintptr_t a = (uintptr_t)(tags + k * pi.tw), e = (uintptr_t)(tags + (k + n) * pi.tw);
+            tw->acquire(a, e);
+            for (uintptr_t x = a; x < e;) {
+                const uintptr_t y = tw->whi(tw->window_of(x)) < e ? tw->whi(tw->window_of(x)) : e;
+                HB_CHECK(hipMemcpyAsync((void *)x, dtags + k * pi.tw + (x - a), (size_t)(y - x), hipMemcpyDeviceToHost,
+                                        c->copy),
+                         "hipMemcpyAsync(D2H tags)");
+                x = y;
+            }
+            tw->release_below(e);
             return 0;
         };
         u64 last_k0 = 0, last_nb = 0;
@@ -1044,6 +1073,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(hipEventSynchronize(c->k1), "encode");
         HB_CHECK(hipEventElapsedTime(&ms_total, c->k0, c->k1), "hipEventElapsedTime");
         if (hw) hw->finish();
+        if (tw) tw->finish();
     }
     c->last_ms = ms_total;
     if (!tags_dev && data_dev)

@@ -58,17 +58,18 @@ extern "C" {
                         caller's stream ("an async variant takes a
                         hipStream_t"). */
 
-#define HB_HOST_REGISTER 32u  /* hb_encode with host data: page-lock the file bytes
-                                 read-only (hipHostRegisterReadOnly) in windows of
-                                 256 MiB, one window ahead of the copy on a helper
-                                 thread, and DMA the chunks straight from them
-                                 (unregistered once copied), instead of the
-                                 runtime's pageable staging.  For read-only
-                                 mappings of files (the reference's file object,
-                                 PySwizzle.py:299) and other large host buffers;
-                                 a window that cannot be registered (e.g. already
-                                 registered by the caller) is copied as is.  Same
-                                 tags. */
+#define HB_HOST_REGISTER 32u  /* hb_encode with host buffers: page-lock the file bytes
+                                 read-only (hipHostRegisterReadOnly) and the host tag
+                                 buffer for writing, in page-aligned windows of
+                                 256 MiB pinned ahead of the copies by helper
+                                 threads, and DMA the chunks straight from / into
+                                 them (each window unpinned once its copies are
+                                 done), instead of the runtime's pageable staging.
+                                 For read-only mappings of files (the reference's
+                                 file object, PySwizzle.py:299) and other large host
+                                 buffers; a window that cannot be registered (e.g.
+                                 already registered by the caller) is copied as is.
+                                 Same tags. */
 
 /* error codes */
 #define HB_OK 0
@@ -111,6 +112,7 @@ const char *hb_build_flags_string(void);
 #define HB_SW_RETRY_CAP 64u
 #define HB_SW_PROVE_BATCH 128u
 #define HB_SW_TRACE_PHASES 256u
+#define HB_SW_HOST_WINDOWS 512u   /* HB_HOST_WINDOW_MIB / HB_HOST_AHEAD: HB_HOST_REGISTER geometry */
 uint32_t hb_test_switches(void);
 
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens

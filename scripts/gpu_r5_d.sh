@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5: HB_HOST_REGISTER with tag windows, real files registered by default:
+# the GPU suite (new tests/test_gpu_hostpath.py) and the default bench line.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r5d}
+mkdir -p $OUT
+step() { local name=$1 limit=$2; shift 2; echo "== $name"; timeout -k 10 $limit "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "   rc=$rc"; tail -1 $OUT/$name.log | cut -c1-400; return $rc; }
+step gpu_tests 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider || exit 1
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
+step bench_c3 600 python -u bench.py || exit 1
+echo done
