@@ -99,6 +99,9 @@ def parse(argv=None):
     ap.add_argument("--prf", default="pyswizzle", choices=["pyswizzle", "cxx"],
                     help="pyswizzle: KeyedPRF, tags bit-exact vs PySwizzle (the headline); cxx: the "
                          "cxx Swizzle extension's PRF (cxx/prf.hxx, CFB-128), parity unpinned")
+    ap.add_argument("--sustain-seconds", type=float, default=6.0,
+                    help="after the timed region, keep encoding the same file for about this long and report "
+                         "the sustained rate (steady-state clock and power; 0 = skip)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the host-memory path rows (4 GiB prefix, after the CPU rows; on by default "
                          "for the N = 1 configs[2] run)")
@@ -349,13 +352,13 @@ def bench_encode(args, cfg, R):
     value = total_bytes / GIB / elapsed
     kernel_ms = sum(kms_list) / len(kms_list)
     achieved_gbs = length / (kernel_ms * 1e-3) / 1e9
-    tries_total = tries_total[0] / args.steps
-    tries_per_block = tries_total / nblocks
+    tries_step = tries_total[0] / args.steps
+    tries_per_block = tries_step / nblocks
     if cxx:
-        aes = tries_total * 2                      # CFB-128 over 32 bytes: 2 full AES per try
+        aes = tries_step * 2                       # CFB-128 over 32 bytes: 2 full AES per try
         lookups = aes * 16 * 14
     else:
-        aes = tries_total * 32                     # nb = 32 byte-0 AES per try
+        aes = tries_step * 32                      # nb = 32 byte-0 AES per try
         if not args.single_pass:
             # the first 4 of every block's first try come from the prefix image,
             # built once per step (2^24 + 2^16 + 2^8 byte-0 AES) per piece
@@ -461,6 +464,8 @@ def bench_encode(args, cfg, R):
         "aes_per_block": round(aes / nblocks, 3),
     }
 
+    if args.sustain_seconds > 0 and len(pieces) == 1:
+        line["sustained"] = sustained(args, R, step, elapsed / args.steps, file_len)
     if not args.no_parity_sample:
         ok, n = parity_sample(ctx, L, dptr, tptr, pieces, plan, S, p, fk, ak, C, w, args, cxx, fill)
         n_all = int(R.reduce(n, "sum"))
@@ -485,6 +490,25 @@ def bench_encode(args, cfg, R):
         print(json.dumps(line), flush=True)
     ctx.check(L.hb_device_free(ctx.h, dptr))
     ctx.check(L.hb_device_free(ctx.h, tptr))
+
+
+def sustained(args, R, step, sec_per_step, file_len):
+    """After the timed region: the same encode step repeated for about
+    --sustain-seconds (the same step count on every rank), timed like the
+    headline (barriers, max over ranks).  A steady-state check -- held clock,
+    socket power at its cap -- of the short timed region, and several seconds
+    of GPU activity for an outside utilisation sampler.  Never `value`."""
+    steps = max(1, int(round(args.sustain_seconds / max(sec_per_step, 1e-6))))
+    R.barrier()
+    t0 = time.perf_counter()
+    kms = 0.0
+    for _ in range(steps):
+        kms += step()[1]
+    R.barrier()
+    el = R.reduce(time.perf_counter() - t0, "max")
+    return {"steps": steps, "seconds": round(el, 3), "value": round(file_len * steps / GIB / el, 3),
+            "unit": "GiB/s", "ms_per_step": round(el / steps * 1e3, 3), "kernel_ms": round(kms / steps, 3),
+            "note": "the timed step repeated after the timed region; not `value`"}
 
 
 def parity_sample(ctx, L, dptr, tptr, pieces, plan, S, p, fk, ak, C, w, args, cxx, fill):
@@ -793,24 +817,39 @@ def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
     p = int.from_bytes(pb, "big")
     out["api_default"] = {"register_kinds": list(pys.REGISTER_KINDS)}
 
-    def api(src, register, reps=2):
-        best = None
+    def api(src, register, reps=3):
+        """Best of `reps` encode_file calls, with the phases of the best one:
+        the FileBuffer (mmap), the encode (hb_encode via encode_shards), and
+        consume + close (munmap)."""
+        from heartbeat_amd import multi
+        from heartbeat_amd._filebuf import FileBuffer
+        best, same = None, True
         for _ in range(reps):
             src.seek(0)
-            t = time.perf_counter()
+            t0 = time.perf_counter()
             tag, _ = pys.encode_file(p, S, fk, ak, src, register=register)
-            dt = time.perf_counter() - t
-            best = dt if best is None else min(best, dt)
-        return n / GIB / best, tag._raw[:nb * 32] == ref.tobytes()
+            dt = time.perf_counter() - t0
+            same = same and tag._raw[:nb * 32] == ref.tobytes()
+            del tag
+            if best is None or dt < best:
+                best = dt
+        # the phases of one more call, spelled out as encode_file does them
+        src.seek(0)
+        t0 = time.perf_counter()
+        fb = FileBuffer(src, populate=not register)
+        t1 = time.perf_counter()
+        tags_out = np.empty(nb * 32, dtype=np.uint8)
+        multi.encode_shards(p, S, fk, ak, fb.addr, fb.len, nb, tags_out.ctypes.data,
+                            _native_flag("HB_HOST_REGISTER") if register else 0, multi.devices())
+        t2 = time.perf_counter()
+        fb.consume()
+        fb.close()
+        t3 = time.perf_counter()
+        phases = {"filebuffer_ms": round((t1 - t0) * 1e3, 2), "encode_ms": round((t2 - t1) * 1e3, 2),
+                  "close_ms": round((t3 - t2) * 1e3, 2)}
+        return n / GIB / best, same, phases
 
     api_ok = True
-    bio = io.BytesIO(host.tobytes())
-    pys.encode_file(p, S, fk, ak, bio)          # warm-up
-    for reg, key in ((False, "api_bytesio_gib_s"), (True, "api_bytesio_register_gib_s")):
-        r, same = api(bio, reg)
-        out[key] = round(r, 3)
-        api_ok = api_ok and same
-    del bio
     with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp")) as fh:
         host.tofile(fh.name)
         # a file at rest (written back, page cache warm), not one still being
@@ -819,12 +858,21 @@ def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
             os.fsync(f.fileno())
             pys.encode_file(p, S, fk, ak, f)
             for reg, key in ((False, "api_file_mmap_gib_s"), (True, "api_file_mmap_register_gib_s")):
-                r, same = api(f, reg, reps=3)
+                r, same, ph = api(f, reg)
                 out[key] = round(r, 3)
+                out[key.replace("_gib_s", "_phases")] = ph
                 api_ok = api_ok and same
             f.seek(0)
             tag, _ = pys.encode_file(p, S, fk, ak, f)
         out["api_prove_file"] = host_file_prove(ctx, L, dptr, pys, p, S, fh.name, n, tag)
+        del tag
+    bio = io.BytesIO(host.tobytes())
+    pys.encode_file(p, S, fk, ak, bio)          # warm-up
+    for reg, key in ((False, "api_bytesio_gib_s"), (True, "api_bytesio_register_gib_s")):
+        r, same, _ = api(bio, reg)
+        out[key] = round(r, 3)
+        api_ok = api_ok and same
+    del bio
     out["api_tags_equal"] = api_ok
     out["unit"] = "GiB/s"
     return out

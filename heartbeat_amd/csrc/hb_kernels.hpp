@@ -1208,17 +1208,20 @@ __device__ __forceinline__ void hb_tree_sum(u32 *sh, u32 n) {
 // the first 2048-bit prove of the process, one workgroup per column, returned
 // a mu of an empty file that was not a sum at all but stale memory (words 0,
 // 16 and 24 = 0x7f / 0x9f / 0x7f, the layout of the engine-queue counters;
-// the same words in two runs with different histories), i.e. the column's
-// finisher had not written out[0 .. NL) in that launch.  (The variant's
-// source was not kept, so the write that broke I1 there is not named here;
-// the shipped kernel keeps I1 by the resets above.)
+// the same words in two runs with different histories): out[0 .. NL) as the
+// host read it was not written by that launch's column finisher -- either the
+// finisher did not run (I1 broken) or its result never reached the host's
+// freshly grown read-back buffer; the data cannot tell which.  (The variant's
+// source was not kept, so the write that broke it is not named here; the
+// shipped kernel keeps I1 by the resets above.)
 // So the host no longer trusts a result the closer did not vouch for: every
 // launch's closer writes out[ncols*NL + 1] = token (distinct per launch,
 // never 0) -- an `accumulate` launch only if the word still holds the
 // previous launch's token (token - 1), else 0 -- and the host rejects the
-// result unless the word equals the last launch's token (finish_sums).  A
-// launch in which some column never finished, or a batch chain with a gap,
-// is thereby a loud error, not a wrong proof.
+// result unless the word equals the last launch's token (finish_sums; the
+// token travels in the same read-back as the sums).  A launch in which some
+// column never finished, a batch chain with a gap, or a read-back that did
+// not land is thereby a loud error, not a wrong proof.
 template <int NL, int ALIGN>
 __global__ __launch_bounds__(HB_WSUM_WG) void hb_wsum_kernel(WsumArgs<NL> A) {
     __shared__ u32 sh[HB_WSUM_WG * (NL + 1)];
