@@ -838,8 +838,8 @@ def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
         t0 = time.perf_counter()
         fb = FileBuffer(src, populate=not register)
         t1 = time.perf_counter()
-        tags_out = np.empty(nb * 32, dtype=np.uint8)
-        multi.encode_shards(p, S, fk, ak, fb.addr, fb.len, nb, tags_out.ctypes.data,
+        tags_out = np.empty((fb.len // C + 1) * 32, dtype=np.uint8)
+        multi.encode_shards(p, S, fk, ak, fb.addr, fb.len, fb.len // C + 1, tags_out.ctypes.data,
                             _native_flag("HB_HOST_REGISTER") if register else 0, multi.devices())
         t2 = time.perf_counter()
         fb.consume()
