@@ -466,6 +466,16 @@ def bench_encode(args, cfg, R):
 
     if args.sustain_seconds > 0 and len(pieces) == 1:
         line["sustained"] = sustained(args, R, step, elapsed / args.steps, file_len)
+    # the host-memory rows come right after the device-resident ones: after
+    # the CPU rows (16 threads streaming 64 GiB through host buffers) the same
+    # rows measured 21-25 instead of 31-38 GiB/s for a real file
+    # (profiles/r05/f: bench_c3 vs bench_c3_nocpu), a state of the process's
+    # host memory, not of the encode
+    want_host = args.host_path or (R.world == 1 and args.config == "c3" and not cxx and not args.single_pass)
+    if R.rank == 0 and want_host and not args.no_host_path:
+        t = time.perf_counter()
+        line["host_path"] = host_path(ctx, L, dptr, pieces[0][1], S, pb, fk, ak, C)
+        line["host_path"]["seconds_spent"] = round(time.perf_counter() - t, 1)
     if not args.no_parity_sample:
         ok, n = parity_sample(ctx, L, dptr, tptr, pieces, plan, S, p, fk, ak, C, w, args, cxx, fill)
         n_all = int(R.reduce(n, "sum"))
@@ -478,13 +488,6 @@ def bench_encode(args, cfg, R):
             fill(0)
         line["cpu_baseline"] = cpu_baseline(ctx, L, dptr, tptr, pieces[0][1], S, p, fk, ak, C,
                                             args.cpu_seconds, args.cpu_threads, args.py_seconds, cxx)
-    want_host = args.host_path or (R.world == 1 and args.config == "c3" and not cxx and not args.single_pass)
-    if R.rank == 0 and want_host and not args.no_host_path:
-        t = time.perf_counter()
-        if len(pieces) > 1:
-            fill(0)
-        line["host_path"] = host_path(ctx, L, dptr, pieces[0][1], S, pb, fk, ak, C)
-        line["host_path"]["seconds_spent"] = round(time.perf_counter() - t, 1)
 
     if R.rank == 0:
         print(json.dumps(line), flush=True)

@@ -363,12 +363,13 @@ class PySwizzle(object):
 
 # Host buffers whose bytes hb_encode page-locks read-only in windows
 # (HB_HOST_REGISTER) instead of staging them through the runtime's pageable
-# copies, by FileBuffer kind.  Real files (read-only mmaps): a 4 GiB file
-# through encode_file measured 42.8 vs 31.7 GiB/s median of 5 on one box
-# (profiles/r05/c/probe6.json, caller-pinned raw rate 49.0); a BytesIO's
-# buffer did not gain (12.5 vs 16.7 in the same run), so it stays pageable.
-# bench.py's host_path measures both ways in every default run.
-REGISTER_KINDS = ("mmap",)
+# copies, by FileBuffer kind: all of them.  A 4 GiB real file through
+# encode_file: 38.2 vs 31.1 GiB/s (registered vs pageable, best of 3), a
+# BytesIO 47.7 vs 43.1, one box (profiles/r05/f/bench_c3_nocpu.log; the
+# caller-pinned raw rate 48.9); the medians of 5 in a standalone probe 40.7 vs
+# 30.4 for the file (profiles/r05/f/probe2.log).  bench.py's host_path
+# measures both ways in every default run.
+REGISTER_KINDS = ("mmap", "bytesio", "bytes", "read")
 
 
 def encode_file(p, sectors, f_key, alpha_key, file, devices=None, register=None):

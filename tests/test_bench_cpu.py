@@ -48,7 +48,7 @@ def test_default_encode_line_with_every_leg(fake, monkeypatch, capsys, tmp_path)
               "api_bytesio_register_gib_s", "api_file_mmap_gib_s", "api_file_mmap_register_gib_s"):
         assert hp[k] > 0, k
     assert set(hp["api_file_mmap_register_phases"]) == {"filebuffer_ms", "encode_ms", "close_ms"}
-    assert hp["api_default"]["register_kinds"] == ["mmap"]
+    assert hp["api_default"]["register_kinds"] == ["mmap", "bytesio", "bytes", "read"]
     # the registered rows really asked the library to register
     from heartbeat_amd import _native
     assert any(f & _native.HB_HOST_REGISTER for f, _ in fake.encodes)
