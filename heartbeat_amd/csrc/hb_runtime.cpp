@@ -636,23 +636,28 @@ int mfma_tables(hb_ctx *c, const Limbs &p, u32 S, u32 kz[17], int layout) {
     return 0;
 }
 
-// HB_HOST_REGISTER: the host bytes [data, data + len) page-locked read-only
+// HB_HOST_REGISTER: host bytes page-locked by the library itself, in
+// page-aligned windows of kWindow bytes -- the file read-only
 // (hipHostRegisterReadOnly: a PROT_READ file mapping cannot be registered for
-// writing) in page-aligned windows of kWindow bytes.  A helper thread
-// registers up to kAhead windows ahead of the chunk being copied -- the page
-// pinning overlaps the DMA of the previous window -- and unregisters each
-// window once the copy-stream event recorded after its last chunk has
-// completed, so at most about kAhead + 2 windows are pinned at a time.  A
-// window whose registration fails (e.g. memory the caller registered
-// already) is simply copied unpinned.  The reference reads the file through
-// Python read() calls (PySwizzle.py:299; cxx/PythonSeekableFile.hxx:47-54);
-// this is the replacement's staging.
+// writing), the tags for writing.  A helper thread registers up to kAhead
+// windows ahead of the chunk being copied -- the page pinning overlaps the
+// DMA of the previous window -- and unregisters each window once the
+// copy-stream event recorded after its last chunk has completed, so at most
+// about kAhead + 2 windows are pinned at a time.  Only pages lying wholly
+// inside the buffer are registered: the partial pages at its two ends (which
+// the neighbouring shard of a multi-device encode, or the caller, may own)
+// are copied unpinned, and every copy is split so that no piece starts in a
+// pinned range and runs past it.  A window whose registration fails (e.g.
+// memory the caller registered already) is copied as is.  The reference
+// reads the file through Python read() calls (PySwizzle.py:299;
+// cxx/PythonSeekableFile.hxx:47-54); this is the replacement's staging.
 struct HostWindows {
     u64 kWindow = 256ull << 20;   // $HB_HOST_WINDOW_MIB (test switch, A/B)
     u64 kAhead = 2;               // $HB_HOST_AHEAD (test switch, A/B)
     enum { NONE = 0, PINNED, UNPINNED, RECORDED, DONE };
     hb_ctx *c;
-    uintptr_t base = 0, end = 0;
+    unsigned int reg_flags;
+    uintptr_t base = 0, end = 0;  // the whole pages inside the buffer
     u64 nwin = 0;
     std::vector<int> state;
     std::vector<hipEvent_t> ev;
@@ -664,7 +669,6 @@ struct HostWindows {
     bool quit = false;
     std::thread th;
 
-    unsigned int reg_flags;
     // host bytes [p, p + len); read_only: the device only reads them (the
     // file), else it writes them (the tags); scale: window size relative to
     // the file's (the tags of a file window: tw / C of it, so that the first
@@ -675,9 +679,10 @@ struct HostWindows {
         if (const char *v = sw_env(c, "HB_HOST_AHEAD")) kAhead = (u64)(atoi(v) > 0 ? atoi(v) : 2);
         kWindow = ((u64)((double)kWindow * scale) + 4095) & ~(u64)4095;
         if (kWindow < (2ull << 20)) kWindow = 2ull << 20;
-        base = (uintptr_t)p & ~(uintptr_t)4095;
-        end = ((uintptr_t)p + len + 4095) & ~(uintptr_t)4095;
-        nwin = len ? (end - base + kWindow - 1) / kWindow : 0;
+        base = ((uintptr_t)p + 4095) & ~(uintptr_t)4095;
+        end = ((uintptr_t)p + len) & ~(uintptr_t)4095;
+        nwin = end > base ? (end - base + kWindow - 1) / kWindow : 0;
+        if (!nwin) end = base;
         state.assign((size_t)nwin, NONE);
         ev.assign((size_t)nwin, nullptr);
         allowed = kAhead + 1;   // start pinning right away, ahead of the first copy
@@ -720,22 +725,23 @@ struct HostWindows {
             cv.wait(lk);
         }
     }
-    // before copying [a, b): allow registration through the window of b plus
-    // kAhead more, and wait until the windows of [a, b) are settled
+    // wait until the windows overlapping [a, b) are settled (registered or
+    // failed), allowing registration kAhead windows further
     void acquire(uintptr_t a, uintptr_t b) {
-        const u64 wb = window_of(b - 1);
+        const uintptr_t lo = a > base ? a : base, hi = b < end ? b : end;
+        if (hi <= lo) return;
+        const u64 wb = window_of(hi - 1);
         std::unique_lock<std::mutex> lk(m);
         if (wb + 1 + kAhead > allowed) {
             allowed = wb + 1 + kAhead;
             cv.notify_all();
         }
         cv.wait(lk, [&] { return next_reg > wb; });
-        (void)a;
     }
-    // every window below the one holding address a is copied for good: record
-    // an event on the copy stream behind those copies, for the helper
-    int release_below(uintptr_t a) {
-        const u64 wa = a >= end ? nwin : window_of(a);
+    // every window wholly below address a is copied for good: record an event
+    // on the copy stream behind those copies, for the helper to unpin it
+    void release_below(uintptr_t a) {
+        const u64 wa = a >= end ? nwin : a <= base ? 0 : window_of(a);
         while (next_rec < wa) {
             const u64 w = next_rec++;
             std::unique_lock<std::mutex> lk(m);
@@ -760,7 +766,24 @@ struct HostWindows {
             }
             cv.notify_all();
         }
-        return 0;
+    }
+    // enqueue the copy of host bytes [a, e) to (h2d) or from the device
+    // memory at dev on the copy stream: one piece per window, the partial
+    // end pages unpinned; windows wholly behind e are handed to the helper
+    hipError_t copy(void *dev, uintptr_t a, uintptr_t e, bool h2d) {
+        acquire(a, e);
+        for (uintptr_t x = a; x < e;) {
+            uintptr_t y = e;
+            if (x < base) y = base < e ? base : e;
+            else if (x < end) y = whi(window_of(x)) < e ? whi(window_of(x)) : e;
+            uint8_t *d = (uint8_t *)dev + (x - a);
+            const hipError_t r = h2d ? hipMemcpyAsync(d, (const void *)x, (size_t)(y - x), hipMemcpyHostToDevice, c->copy)
+                                     : hipMemcpyAsync((void *)x, d, (size_t)(y - x), hipMemcpyDeviceToHost, c->copy);
+            if (r != hipSuccess) return r;
+            x = y;
+        }
+        release_below(e);
+        return hipSuccess;
     }
     // stop the helper; every window still pinned is unpinned after the copy
     // stream has drained (all exit paths, errors included)
@@ -1015,16 +1038,9 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
                 return 0;
             }
             // pinned tag windows: one DMA per window piece
-            const uintptr_t a = (uintptr_t)(tags + k * pi.tw), e = (uintptr_t)(tags + (k + n) * pi.tw);
-            tw->acquire(a, e);
-            for (uintptr_t x = a; x < e;) {
-                const uintptr_t y = tw->whi(tw->window_of(x)) < e ? tw->whi(tw->window_of(x)) : e;
-                HB_CHECK(hipMemcpyAsync((void *)x, dtags + k * pi.tw + (x - a), (size_t)(y - x), hipMemcpyDeviceToHost,
-                                        c->copy),
-                         "hipMemcpyAsync(D2H tags)");
-                x = y;
-            }
-            tw->release_below(e);
+            HB_CHECK(tw->copy(dtags + k * pi.tw, (uintptr_t)(tags + k * pi.tw), (uintptr_t)(tags + (k + n) * pi.tw),
+                              false),
+                     "hipMemcpyAsync(D2H tags)");
             return 0;
         };
         u64 last_k0 = 0, last_nb = 0;
@@ -1037,16 +1053,8 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             if (it >= 2) HB_CHECK(hipStreamWaitEvent(c->copy, c->done[b], 0), "hipStreamWaitEvent");
             if (bytes && hw) {
                 // pinned windows: one DMA per window piece of the chunk
-                const uintptr_t a = (uintptr_t)(data + off), e = (uintptr_t)(data + end);
-                hw->acquire(a, e);
-                for (uintptr_t x = a; x < e;) {
-                    const uintptr_t y = hw->whi(hw->window_of(x)) < e ? hw->whi(hw->window_of(x)) : e;
-                    HB_CHECK(hipMemcpyAsync((uint8_t *)c->data[b].p + (x - a), (const void *)x, (size_t)(y - x),
-                                            hipMemcpyHostToDevice, c->copy),
-                             "hipMemcpyAsync(H2D)");
-                    x = y;
-                }
-                hw->release_below(e);
+                HB_CHECK(hw->copy(c->data[b].p, (uintptr_t)(data + off), (uintptr_t)(data + end), true),
+                         "hipMemcpyAsync(H2D)");
             } else if (bytes) {
                 HB_CHECK(hipMemcpyAsync(c->data[b].p, data + off, (size_t)bytes, hipMemcpyHostToDevice, c->copy),
                          "hipMemcpyAsync(H2D)");
