@@ -1,7 +1,7 @@
 """Provenance of the committed measurement records (CPU): the traffic figure
 bench.py quotes (profiles/pmc_traffic.json, roofline.traffic) is exactly what
 scripts/pmc_traffic.py derives from the committed rocprofv3 --pmc passes it
-names, and every profile file DESIGN.md cites for round 4 exists."""
+names, and every profile file DESIGN.md cites for rounds 4 and 5 exists."""
 import json
 import os
 import re
@@ -22,9 +22,10 @@ def test_pmc_traffic_reproduces_from_committed_passes():
         assert again[k] == rec[k], k
 
 
-def test_design_cites_existing_round4_profiles():
+def test_design_cites_existing_round4_and_round5_profiles():
     text = open(os.path.join(ROOT, "DESIGN.md")).read()
-    cited = set(re.findall(r"`(profiles/r04/[^`*{}\n]+?)`", text))
-    assert cited
-    missing = [c for c in cited if not os.path.exists(os.path.join(ROOT, c.rstrip("/").split(" ")[0]))]
-    assert not missing, missing
+    for rnd in ("r04", "r05"):
+        cited = set(re.findall(r"`(profiles/%s/[^`*{}\n]+?)`" % rnd, text))
+        assert cited, rnd
+        missing = [c for c in cited if not os.path.exists(os.path.join(ROOT, c.rstrip("/").split(" ")[0]))]
+        assert not missing, missing
