@@ -6,11 +6,15 @@ host-memory rows, JSON line -- before they cost a GPU run.  Numbers are
 meaningless here; only the structure and the built-in cross-checks are
 asserted."""
 import json
+import os
+import socket
+import subprocess
 import sys
 
 import pytest
 
 import fake_native
+from conftest import ROOT
 
 
 @pytest.fixture
@@ -67,3 +71,32 @@ def test_prove_line(fake, monkeypatch, capsys):
     assert d["unit"] == "ms" and d["higher_is_better"] is False
     assert d["proof_equal_oracle"] is True
     assert d["cpu_baseline"]["proof_equal_gpu"] is True
+
+
+def test_two_rank_encode_line(tmp_path):
+    """Two ranks (gloo, one process each) of the c4 plan through the stand-in
+    library: every leg that runs at N > 1 -- shard plan, timed loop with
+    barriers and max-over-ranks, sustained leg, per-rank parity sample summed
+    over ranks -- and exactly one JSON line from rank 0."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TMPDIR=str(tmp_path))
+        env.pop("HB_BENCH_SAME_DEVICE", None)
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(ROOT, "tests", "run_bench_fake.py"), "--gpus", "2", "--gib", "0.001",
+             "--steps", "2", "--warmup", "1", "--sustain-seconds", "0.05", "--parity-blocks", "50"],
+            env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["workload"].startswith("configs[3]")
+    assert d["parity_sample"]["ok"] is True and d["sustained"]["steps"] >= 1
+    assert "host_path" not in d and "cpu_baseline" not in d
