@@ -14,6 +14,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <condition_variable>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1026,9 +1027,14 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(c->data[0].ensure((size_t)(cb * C)), "hipMalloc(staging)");
         HB_CHECK(c->data[1].ensure((size_t)(cb * C)), "hipMalloc(staging)");
         std::unique_ptr<HostWindows> hw, tw;
-        if ((flags & HB_HOST_REGISTER) && len) hw.reset(new HostWindows(c, data, len, true));
-        if ((flags & HB_HOST_REGISTER) && !tags_dev)
-            tw.reset(new HostWindows(c, tags, nblocks * pi.tw, false, (double)pi.tw / (double)C));
+        try {   // (a helper thread that cannot be started: copy unpinned)
+            if ((flags & HB_HOST_REGISTER) && len) hw.reset(new HostWindows(c, data, len, true));
+            if ((flags & HB_HOST_REGISTER) && !tags_dev)
+                tw.reset(new HostWindows(c, tags, nblocks * pi.tw, false, (double)pi.tw / (double)C));
+        } catch (const std::exception &) {
+            hw.reset();
+            tw.reset();
+        }
         auto tags_back = [&](u64 k, u64 n, int buf) -> int {
             HB_CHECK(hipStreamWaitEvent(c->copy, c->done[buf], 0), "hipStreamWaitEvent");
             if (!tw) {
