@@ -144,6 +144,17 @@ struct ProveArgs {
     unsigned long long *queue;    // 2 slots: index engine, v engine
     unsigned int *flags;          // bit 0: an index >= #tags (cxx prf after 81 tries)
     u64 qchunk;                   // jobs per queue refill
+    // Device gather (device-resident file and tags): as each index is found,
+    // block idx_i's S sectors (full ss-byte integers) and tag are copied to
+    // slot i of gdata / gtags, the layout of the host gather, so that the
+    // weighted sum reads one compact buffer (wsum mode 2).  gdata == nullptr: off.
+    const unsigned char *data;    // the file (len bytes) and the tags (ntags x tw)
+    u64 len, C;
+    u32 ss, S, tw;
+    u32 galign16;                 // data, C and gdata allow whole-block 16-byte copies
+    const unsigned char *tags;
+    unsigned char *gdata;         // n x C
+    unsigned char *gtags;         // n x tw
 };
 
 // Weighted sums  sum_i w_i * value_{col}(i)  mod p  (w_i in Montgomery form);

@@ -1066,6 +1066,40 @@ __global__ __launch_bounds__(256) void hb_mont_kernel(MontArgs<NL> A) {
 // 762, 767) for i < n in ONE launch: two engine runs over the same LDS image,
 // v stored in Montgomery form (v R mod p) for stage 2.  check_all (cxx prove
 // with a challenge covering every block, :754-762) skips the index PRF.
+// Block ix of the file -- its S sectors as full ss-byte big-endian integers
+// (a short last sector right-aligned, sectors past EOF zero: the reference's
+// seek/read per sector, PySwizzle.py:353-360) and its tag -- copied to slot
+// job of the compact gather buffers: the device twin of the host gather
+// (hb_runtime.cpp, Gather::run).  One lane; whole-block 16-byte copies when
+// the block lies inside the file and everything is 16-byte aligned.
+__device__ __forceinline__ void hb_gather_block(const unsigned char *data, u64 len, u64 C, u32 ss, u32 S,
+                                                const unsigned char *tags, u32 tw, u64 ntags, u32 align16,
+                                                unsigned char *gdata, unsigned char *gtags, u64 job, u64 ix) {
+    unsigned char *dst = gdata + job * C;
+    unsigned char *tdst = gtags + job * (u64)tw;
+    if (ix >= ntags) {   // reported by the host (flags); summed as 0
+        for (u64 b = 0; b < C; ++b) dst[b] = 0;
+        for (u32 b = 0; b < tw; ++b) tdst[b] = 0;
+        return;
+    }
+    const u64 base = ix * C;
+    if (align16 && base + C <= len) {
+        const uint4 *s = reinterpret_cast<const uint4 *>(data + base);
+        uint4 *d = reinterpret_cast<uint4 *>(dst);
+        for (u64 k = 0; k < C / 16; ++k) d[k] = s[k];
+    } else {
+        for (u32 j = 0; j < S; ++j) {
+            const u64 pos = base + (u64)j * ss;
+            const u64 r = pos >= len ? 0 : (len - pos < ss ? len - pos : ss);
+            unsigned char *ds = dst + (u64)j * ss;
+            for (u64 b = 0; b < ss - r; ++b) ds[b] = 0;
+            for (u64 b = 0; b < r; ++b) ds[ss - r + b] = data[pos + b];
+        }
+    }
+    const unsigned char *ts = tags + ix * (u64)tw;
+    for (u32 b = 0; b < tw; ++b) tdst[b] = ts[b];
+}
+
 template <int NL>
 struct ProveIdxHandler {
     const ProveArgs<NL> &A;
@@ -1078,6 +1112,10 @@ struct ProveIdxHandler {
         // on which the reference's t.sigma().at(index) throws: flagged here,
         // raised by the host; stage 2 reads such a term as 0
         if (ix >= A.ntags) atomicOr(A.flags, 1u);
+        // gather the challenged block while the v chains are still running
+        if (A.gdata)
+            hb_gather_block(A.data, A.len, A.C, A.ss, A.S, A.tags, A.tw, A.ntags, A.galign16, A.gdata, A.gtags, job,
+                            ix);
     }
 };
 

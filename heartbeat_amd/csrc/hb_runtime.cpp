@@ -98,6 +98,7 @@ struct hb_ctx {
     DevBuf afrag;        // MFMA MAC: digit fragments of alpha_j R mod p
     DevBuf ctl;          // wsum column counters + flags (zero between operations)
     DevBuf mseeds, moffs, mdig;   // Merkle chunk seeds, offsets, HMAC digests
+    DevBuf gdev;         // device-resident prove: the challenged blocks and tags, gathered
     HostBuf gstage[2];   // host-file prove: pinned gather buffers (blocks | tags), double-buffered
     HostBuf hscratch;    // pinned staging of the encode's small host round trips (alpha, MFMA tables)
     // the alpha D2H into hscratch done / the MFMA-table H2D out of it done
@@ -177,6 +178,7 @@ const SwitchName kSwitches[] = {
     {"HB_TRACE_PHASES", HB_SW_TRACE_PHASES},
     {"HB_HOST_WINDOW_MIB", HB_SW_HOST_WINDOWS},
     {"HB_HOST_AHEAD", HB_SW_HOST_WINDOWS},
+    {"HB_NO_PROVE_GATHER", HB_SW_NO_PROVE_GATHER},
 };
 
 int nl_for_bits(int bits) {
@@ -1325,6 +1327,28 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         tags = (const uint8_t *)c->tags.p;
         tags_dev = true;
     }
+    // Device-resident file and tags: the PRF kernel gathers each challenged
+    // block and tag into a compact buffer as soon as its index is found
+    // (hb_gather_block, under the still-running v chains), and the weighted
+    // sum reads that buffer (mode 2) instead of n random blocks of the file.
+    // PySwizzle mode (no check_all), up to 64 MiB of gathered bytes;
+    // $HB_NO_PROVE_GATHER (test switch, A/B) keeps the file-gathering sum.
+    const u64 gstride = (n * C + 15) & ~15ull;
+    const bool dev_gather = data_dev && tags_dev && !cxx && !check_all && !sw_env(c, "HB_NO_PROVE_GATHER") &&
+                            n * (C + pi.tw) <= (64ull << 20);
+    if (dev_gather) {
+        HB_CHECK(c->gdev.ensure((size_t)(gstride + n * pi.tw)), "hipMalloc(gather)");
+        PA.data = data;
+        PA.len = len;
+        PA.C = C;
+        PA.ss = pi.ss;
+        PA.S = S;
+        PA.tw = pi.tw;
+        PA.tags = tags;
+        PA.gdata = (unsigned char *)c->gdev.p;
+        PA.gtags = (unsigned char *)c->gdev.p + gstride;
+        PA.galign16 = ((uintptr_t)data % 16 == 0 && C % 16 == 0) ? 1u : 0u;
+    }
     // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
     const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
     HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, quad ? 3 : mode_i, quad ? 3 : mode_v, pgrid, c->stream),
@@ -1345,7 +1369,18 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     A.qslots = PA.queue;
     A.nslots = 2;
     int rc = 0;
-    if (data_dev && tags_dev) {
+    if (dev_gather) {
+        A.mode = 2;
+        A.w = (const u32 *)c->wts.p;
+        A.nterms = n;
+        A.data = PA.gdata;
+        A.len = n * C;
+        A.tags = PA.gtags;
+        A.finalize = 1;
+        rc = launch_wsum<NL>(c, A, full16(pi, NL, C, PA.gdata) ? 16 : 1);
+        if (rc) return rc;
+        c->last_launches++;
+    } else if (data_dev && tags_dev) {
         A.mode = 0;
         A.idx = check_all ? nullptr : (const u64 *)c->idx.p;
         A.idx_base = chunk_begin;
@@ -1611,7 +1646,7 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
                       &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
-                      &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig};
+                      &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig, &c->gdev};
     for (DevBuf *b : bufs) b->release();
     if (c->hres) (void)hipHostFree(c->hres);
     c->gstage[0].release();

@@ -113,6 +113,7 @@ const char *hb_build_flags_string(void);
 #define HB_SW_PROVE_BATCH 128u
 #define HB_SW_TRACE_PHASES 256u
 #define HB_SW_HOST_WINDOWS 512u   /* HB_HOST_WINDOW_MIB / HB_HOST_AHEAD: HB_HOST_REGISTER geometry */
+#define HB_SW_NO_PROVE_GATHER 1024u  /* HB_NO_PROVE_GATHER: device proves sum straight from the file */
 uint32_t hb_test_switches(void);
 
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens

@@ -110,3 +110,54 @@ def test_alternating_proves_and_verifies_on_one_context(oracle, monkeypatch):
     finally:
         for b in bufs:
             ctx.check(L.hb_device_free(ctx.h, b))
+
+
+@pytest.mark.parametrize("pname,S,n,chunks,misalign", [
+    ("p256", 16, (8 << 20) + 77, 10000, 0),     # whole-block 16-byte gathers, ragged tail block
+    ("p256", 16, (1 << 20) + 5, 3000, 3),       # misaligned file: every block gathered sector by sector
+    ("p255", 10, 123457, 2000, 0),              # 31-byte sectors, C = 310 (not a multiple of 16)
+    ("p2048", 3, 40000, 5000, 0),               # 2048-bit: C = 768, partial last block
+    ("p256", 1, 0, 5, 0),                       # empty file: every sector past EOF
+])
+def test_device_gather_equals_file_sum(oracle, monkeypatch, pname, S, n, chunks, misalign):
+    """A device-resident prove gathers each challenged block and tag in the
+    PRF kernel (hb_gather_block) and sums the compact buffer; the same prove
+    with the gather off (HB_NO_PROVE_GATHER, the sum reads the file directly)
+    and the oracle agree.  Reference: PySwizzle.py:351-368."""
+    from heartbeat_amd import _native as nat
+    ctx = nat.context()
+    L = nat.lib()
+    p = _primes()[pname]
+    w = nat.width_of(p)
+    C = (p.bit_length() // 8) * S
+    rng = np.random.default_rng(n + S)
+    data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    fk, ak = b"g" * 32, b"h" * 32
+    tags = oracle.encode(p, S, fk, ak, data, nthreads=8)
+    nb = len(tags)
+    traw = np.frombuffer(b"".join(t.to_bytes(w, "big") for t in tags), dtype=np.uint8)
+    dd, dt = ctypes.c_void_p(), ctypes.c_void_p()
+    ctx.check(L.hb_device_malloc(ctx.h, n + 64, ctypes.byref(dd)))
+    ctx.check(L.hb_device_malloc(ctx.h, len(traw), ctypes.byref(dt)))
+    try:
+        dptr = dd.value + misalign
+        if n:
+            hd = np.frombuffer(data, dtype=np.uint8)
+            ctx.check(L.hb_memcpy(ctx.h, dptr, hd.ctypes.data, n, 1))
+        ctx.check(L.hb_memcpy(ctx.h, dt, traw.ctypes.data, len(traw), 1))
+        key = hashlib.sha256(b"gather%d" % n).digest()
+        pb = nat.be(p)
+        res = []
+        for off in (False, True):
+            if off:
+                monkeypatch.setenv("HB_NO_PROVE_GATHER", "1")
+            mu = ctypes.create_string_buffer(w * S)
+            sg = ctypes.create_string_buffer(w)
+            ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, key, 32, chunks, pb, len(pb), dt, nb, dptr, n, 3, mu, sg))
+            res.append((_ints(mu.raw, w, S), int.from_bytes(sg.raw, "big")))
+        monkeypatch.delenv("HB_NO_PROVE_GATHER", raising=False)
+        assert res[0] == res[1]
+        assert res[0] == oracle.prove(p, S, key, chunks, p, tags, data)
+    finally:
+        ctx.check(L.hb_device_free(ctx.h, dd))
+        ctx.check(L.hb_device_free(ctx.h, dt))
