@@ -112,7 +112,11 @@ struct hb_ctx {
     // HB_ENABLE_TEST_SWITCHES=1 when the context was created: the A/B and test
     // switches (sw_env) are honoured; otherwise none is even read
     bool switches = false;
-    u32 *hres = nullptr; // pinned host copy of wsum results (+ status)
+    u32 *hres = nullptr; // pinned host buffer of the wsum results (+ status, token)
+    bool sums_in_hres = true;   // the last wsum wrote its results straight into hres
+    // R^2 mod p (Montgomery conversion) of the last prime seen: ~10 us of host
+    // big-integer work per call otherwise, on a prove's critical path
+    Limbs r2_p, r2_val;
     size_t hres_n = 0;
     std::string err;
     double last_ms = 0.0;
@@ -179,6 +183,7 @@ const SwitchName kSwitches[] = {
     {"HB_HOST_WINDOW_MIB", HB_SW_HOST_WINDOWS},
     {"HB_HOST_AHEAD", HB_SW_HOST_WINDOWS},
     {"HB_NO_PROVE_GATHER", HB_SW_NO_PROVE_GATHER},
+    {"HB_SUMS_ON_DEVICE", HB_SW_SUMS_ON_DEVICE},
 };
 
 int nl_for_bits(int bits) {
@@ -215,6 +220,15 @@ void make_mod(const Limbs &p, ModP<NL> &M) {
     for (int t = 0; t < NL; ++t) M.p[t] = p[t];
     M.pinv = mont_pinv(p[0]);
     M.inv_scaled = inv_scaled(p);
+}
+
+// R^2 mod p for NL limbs (R = 2^(32 NL)), cached per context for the last p.
+const Limbs &r2_of(hb_ctx *c, const Limbs &p, int nl) {
+    if (c->r2_p != p || c->r2_val.size() != (size_t)nl) {
+        c->r2_val = pow2_mod(64u * (unsigned)nl, p);
+        c->r2_p = p;
+    }
+    return c->r2_val;
 }
 
 int engine_grid(hb_ctx *c, u64 njobs) {
@@ -301,7 +315,7 @@ int run_mont(hb_ctx *c, const Limbs &p, const u32 *in, u32 *out, u64 n) {
     if (n == 0) return 0;
     MontArgs<NL> A;
     make_mod<NL>(p, A.mod);
-    Limbs r2 = pow2_mod(64u * NL, p);
+    const Limbs &r2 = r2_of(c, p, NL);
     for (int t = 0; t < NL; ++t) A.r2[t] = r2[t];
     A.in = in;
     A.out = out;
@@ -1161,7 +1175,18 @@ int launch_wsum(hb_ctx *c, WsumArgs<NL> &A, int align) {
     A.partials = (u32 *)c->partials.p;
     A.ctl = (unsigned int *)c->ctl.p;
     A.flags = flags_word(c);
-    A.out = (u32 *)c->sums.p;
+    // The finishers write the results (ncols values, status, token) straight
+    // into the pinned host buffer the caller's values are read from: no D2H
+    // copy (a blit launch and its latency, ~10 us of a ~0.22 ms prove) after
+    // the sum.  $HB_SUMS_ON_DEVICE (test switch, A/B): device buffer + copy.
+    const size_t words = (size_t)A.ncols * NL + 2;
+    c->sums_in_hres = !sw_env(c, "HB_SUMS_ON_DEVICE");
+    if (c->sums_in_hres) {
+        if (int rc = ensure_hres(c, words)) return rc;
+        A.out = c->hres;
+    } else {
+        A.out = (u32 *)c->sums.p;
+    }
     A.token = next_token(c, !A.accumulate);
     HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");
     return 0;
@@ -1173,8 +1198,12 @@ int launch_wsum(hb_ctx *c, WsumArgs<NL> &A, int align) {
 template <int NL>
 int finish_sums(hb_ctx *c, u32 ncols, u32 tw, uint8_t *out, bool cxx_index_check) {
     const size_t words = (size_t)ncols * NL + 2;
-    if (int rc = ensure_hres(c, words)) return rc;
-    HB_CHECK(hipMemcpyAsync(c->hres, c->sums.p, words * 4, hipMemcpyDeviceToHost, c->stream), "hipMemcpy");
+    if (!c->sums_in_hres) {
+        if (int rc = ensure_hres(c, words)) return rc;
+        HB_CHECK(hipMemcpyAsync(c->hres, c->sums.p, words * 4, hipMemcpyDeviceToHost, c->stream), "hipMemcpy");
+    }
+    // (a polled wait -- hipEventQuery in a loop -- measured slower than this
+    // blocking one: 0.2118 vs 0.2041 ms per configs[4] proof, profiles/r05/j)
     HB_CHECK(hipStreamSynchronize(c->stream), "prove");
     if (c->hres[(size_t)ncols * NL + 1] != c->wsum_token) {
         // some column's finisher (or a batch) did not run: out[] is not this
@@ -1293,7 +1322,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     if (!make_prf<2>(chal_key, key_len, nbe, 8, PA.pi, nr2) || !make_prf<NL>(chal_key, key_len, vmax_be, vmax_len, PA.pv, nr))
         return fail(c, HB_EINVAL, "invalid challenge key");
     make_mod<NL>(p, PA.mod);
-    Limbs r2 = pow2_mod(64u * NL, p);
+    const Limbs &r2 = r2_of(c, p, NL);
     for (int t = 0; t < NL; ++t) PA.r2[t] = r2[t];
     HB_CHECK(c->idx.ensure((size_t)n * 8), "hipMalloc(idx)");
     HB_CHECK(c->wts.ensure((size_t)n * NL * 4), "hipMalloc(v)");
