@@ -151,7 +151,7 @@ struct ProveArgs {
     const unsigned char *data;    // the file (len bytes) and the tags (ntags x tw)
     u64 len, C;
     u32 ss, S, tw;
-    u32 galign16;                 // data, C and gdata allow whole-block 16-byte copies
+    u32 galign16;                 // file, tags, C and tw allow 16-byte copies
     const unsigned char *tags;
     unsigned char *gdata;         // n x C
     unsigned char *gtags;         // n x tw

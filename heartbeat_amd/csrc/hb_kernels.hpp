@@ -1084,9 +1084,19 @@ __device__ __forceinline__ void hb_gather_block(const unsigned char *data, u64 l
     }
     const u64 base = ix * C;
     if (align16 && base + C <= len) {
+        // eight 16-byte loads in flight before their stores
         const uint4 *s = reinterpret_cast<const uint4 *>(data + base);
         uint4 *d = reinterpret_cast<uint4 *>(dst);
-        for (u64 k = 0; k < C / 16; ++k) d[k] = s[k];
+        const u64 nq = C / 16;
+        for (u64 k = 0; k < nq; k += 8) {
+            uint4 v[8];
+            HB_UNROLL
+            for (int j = 0; j < 8; ++j)
+                if (k + j < nq) v[j] = s[k + j];
+            HB_UNROLL
+            for (int j = 0; j < 8; ++j)
+                if (k + j < nq) d[k + j] = v[j];
+        }
     } else {
         for (u32 j = 0; j < S; ++j) {
             const u64 pos = base + (u64)j * ss;
@@ -1097,7 +1107,12 @@ __device__ __forceinline__ void hb_gather_block(const unsigned char *data, u64 l
         }
     }
     const unsigned char *ts = tags + ix * (u64)tw;
-    for (u32 b = 0; b < tw; ++b) tdst[b] = ts[b];
+    if (align16) {   // tw % 16 == 0 and 16-byte aligned tags (hb_runtime.cpp)
+        for (u32 q = 0; q < tw / 16; ++q)
+            reinterpret_cast<uint4 *>(tdst)[q] = reinterpret_cast<const uint4 *>(ts)[q];
+    } else {
+        for (u32 b = 0; b < tw; ++b) tdst[b] = ts[b];
+    }
 }
 
 template <int NL>

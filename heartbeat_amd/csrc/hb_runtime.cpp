@@ -1360,11 +1360,15 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     // block and tag into a compact buffer as soon as its index is found
     // (hb_gather_block, under the still-running v chains), and the weighted
     // sum reads that buffer (mode 2) instead of n random blocks of the file.
-    // PySwizzle mode (no check_all), up to 64 MiB of gathered bytes;
-    // $HB_NO_PROVE_GATHER (test switch, A/B) keeps the file-gathering sum.
+    // PySwizzle mode (no check_all), up to 64 MiB of gathered bytes, and
+    // layouts the gather copies in 16-byte pieces (file, tags, C and the tag
+    // width 16-byte aligned: one lane copying a block byte by byte would
+    // outlast the v chains); $HB_NO_PROVE_GATHER (test switch, A/B) keeps the
+    // file-gathering sum.
     const u64 gstride = (n * C + 15) & ~15ull;
-    const bool dev_gather = data_dev && tags_dev && !cxx && !check_all && !sw_env(c, "HB_NO_PROVE_GATHER") &&
-                            n * (C + pi.tw) <= (64ull << 20);
+    const bool galign16 = (uintptr_t)data % 16 == 0 && (uintptr_t)tags % 16 == 0 && C % 16 == 0 && pi.tw % 16 == 0;
+    const bool dev_gather = data_dev && tags_dev && !cxx && !check_all && galign16 &&
+                            !sw_env(c, "HB_NO_PROVE_GATHER") && n * (C + pi.tw) <= (64ull << 20);
     if (dev_gather) {
         HB_CHECK(c->gdev.ensure((size_t)(gstride + n * pi.tw)), "hipMalloc(gather)");
         PA.data = data;
@@ -1376,7 +1380,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         PA.tags = tags;
         PA.gdata = (unsigned char *)c->gdev.p;
         PA.gtags = (unsigned char *)c->gdev.p + gstride;
-        PA.galign16 = ((uintptr_t)data % 16 == 0 && C % 16 == 0) ? 1u : 0u;
+        PA.galign16 = 1u;
     }
     // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
     const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;

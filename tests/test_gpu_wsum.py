@@ -114,16 +114,19 @@ def test_alternating_proves_and_verifies_on_one_context(oracle, monkeypatch):
 
 @pytest.mark.parametrize("pname,S,n,chunks,misalign", [
     ("p256", 16, (8 << 20) + 77, 10000, 0),     # whole-block 16-byte gathers, ragged tail block
-    ("p256", 16, (1 << 20) + 5, 3000, 3),       # misaligned file: every block gathered sector by sector
-    ("p255", 10, 123457, 2000, 0),              # 31-byte sectors, C = 310 (not a multiple of 16)
+    ("p256", 16, (1 << 20) + 5, 3000, 3),       # misaligned file: the file sum (no gather)
+    ("p255", 10, 123457, 2000, 0),              # 31-byte sectors, C = 310: the file sum (no gather)
     ("p2048", 3, 40000, 5000, 0),               # 2048-bit: C = 768, partial last block
     ("p256", 1, 0, 5, 0),                       # empty file: every sector past EOF
 ])
 def test_device_gather_equals_file_sum(oracle, monkeypatch, pname, S, n, chunks, misalign):
     """A device-resident prove gathers each challenged block and tag in the
-    PRF kernel (hb_gather_block) and sums the compact buffer; the same prove
-    with the gather off (HB_NO_PROVE_GATHER, the sum reads the file directly)
-    and the oracle agree.  Reference: PySwizzle.py:351-368."""
+    PRF kernel (hb_gather_block: 16-byte copies for whole blocks, sector by
+    sector for the ragged last block and past EOF) and sums the compact buffer;
+    the same prove with the gather off (HB_NO_PROVE_GATHER, the sum reads the
+    file directly) and the oracle agree.  Layouts the gather does not take
+    (misaligned file, C = 310) run the file sum either way.
+    Reference: PySwizzle.py:351-368."""
     from heartbeat_amd import _native as nat
     ctx = nat.context()
     L = nat.lib()
