@@ -1339,7 +1339,8 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     const int vnb = (bitlen_be(vmax_be, vmax_len) + 7) / 8;
     const int mode_i = cxx ? 2 : 0, mode_v = cxx ? (vnb % 16 ? 2 : 1) : 0;
     c->last_launches = 0;
-    HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
+    // (no timing events: hb_last_kernel_ms reports encodes, and a prove is
+    // latency-bound -- every host API call is on its critical path)
     c->prove_dirty = true;
     const bool quad = !cxx && use_quad(c, 2 * n);
     const EngineShape es = quad ? quad_engine(c, 2 * n) : small_engine(c, 2 * n);
@@ -1493,16 +1494,12 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
             c->last_launches++;
         }
     }
-    HB_CHECK(hipEventRecord(c->k1, c->stream), "hipEventRecord");
     std::vector<uint8_t> out((size_t)ncols * pi.tw);
     rc = finish_sums<NL>(c, ncols, pi.tw, out.data(), cxx && !check_all);
     // the finalizing launch ran to its end (its status decides rc) unless the
     // completion token says otherwise: then its PRF slots were not cleared
     c->prove_dirty = c->ctl_dirty;
     if (rc) return rc;
-    float ms = 0.f;
-    HB_CHECK(hipEventElapsedTime(&ms, c->k0, c->k1), "hipEventElapsedTime");
-    c->last_ms = ms;
     memcpy(mu_out, out.data(), (size_t)S * pi.tw);
     memcpy(sigma_out, out.data() + (size_t)S * pi.tw, pi.tw);
     return 0;
