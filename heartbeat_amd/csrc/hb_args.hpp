@@ -144,6 +144,7 @@ struct ProveArgs {
     unsigned long long *queue;    // 2 slots: index engine, v engine
     unsigned int *flags;          // bit 0: an index >= #tags (cxx prf after 81 tries)
     u64 qchunk;                   // jobs per queue refill
+    u32 place;                    // quad engine: waves placed by SIMD (hb_prove_place), no queue
     // Device gather (device-resident file and tags): as each index is found,
     // block idx_i's S sectors (full ss-byte integers) and tag are copied to
     // slot i of gdata / gtags, the layout of the host gather, so that the

@@ -309,10 +309,11 @@ __device__ __forceinline__ u32 hb_quad_prf_try(const QuadLane &Q, const u32 *rkq
 // hb_engine (MODE 0, fresh evaluations: h.init zeroes the register) with one
 // job per quad.  Only lane q = 0 of a quad takes jobs and calls h.accept; the
 // job index is broadcast to the quad.  `chunk` = jobs per refill per wave
-// (16 = one per quad).
+// (16 = one per quad).  `first` != ~0: the wave runs jobs [first, first + 16)
+// and never touches the queue (placed waves, hb_prove_place).
 template <int NL, int NR, class H>
 __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const PrfParams<NL> &P, u64 njobs,
-                                               unsigned long long *queue, u64 chunk) {
+                                               unsigned long long *queue, u64 chunk, u64 first = ~0ull) {
     const QuadLane Q = hb_quad_lane(L);
     const u32 q = hb_lane_id() & 3u;
     const bool lead = q == 0;
@@ -326,7 +327,8 @@ __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const Prf
         const u32 k2 = __builtin_amdgcn_readfirstlane(P.rk[4 * r + 2]), k3 = __builtin_amdgcn_readfirstlane(P.rk[4 * r + 3]);
         rkq[r] = q == 0 ? k0 : q == 1 ? k1 : q == 2 ? k2 : k3;
     }
-    HbPool pool{0, 0, njobs, queue, false, chunk};
+    HbPool pool = first == ~0ull ? HbPool{0, 0, njobs, queue, false, chunk}
+                                 : HbPool{first, njobs - first < 16 ? njobs : first + 16, njobs, queue, true, chunk};
     u64 job = 0;
     bool active = pool.take(__ballot(lead), lead, job);
     job = hb_qbcast64(job);
@@ -1147,11 +1149,66 @@ struct ProveVHandler {
     }
 };
 
+// Static placement of a prove's quad-engine waves (A.place).  The launch
+// lasts as long as its longest v chain, and a wave sharing its SIMD with
+// other busy waves runs its chain up to 1.5x slower (one wave: 1,468 clocks
+// per CFB-8 step; four on one SIMD: up to 2,202, scripts/ubench_latency.hip),
+// so instead of racing for the job queue, each wave is given 16 jobs by
+// position: v waves (nb CFB-8 steps per try) one per SIMD where they fit,
+// index waves (4 steps per try for up to 2^32 tags) on the remaining SIMDs,
+// two or more to a SIMD if they must.  Waves 4m .. 4m+3 of a workgroup run on
+// the CU's four SIMDs (HW_ID, scripts/ubench_hwid.hip): slot s = (w & 3) * G
+// + g is one SIMD and layer w >> 2 a wave on it.  Segregated when the v waves
+// fit one layer and the index waves the free slots' four layers; otherwise
+// balanced: v positions fill slots upward, index positions downward, which
+// stacks at most ceil((nv + ni) / 4G) <= 4 waves on a slot (the host places
+// only when nv + ni <= 16 G).  Returns 1 (v), 2 (index) or 0 (no jobs) and
+// the wave's first job.
+__device__ __forceinline__ int hb_prove_place(u32 G, u32 g, u32 w, u64 n, bool idx_too, u64 &first) {
+    const u64 S4 = 4ull * G, s = (u64)(w & 3u) * G + g, layer = w >> 2;
+    const u64 nv = (n + 15) / 16, ni = idx_too ? nv : 0;
+    const u64 F = nv < S4 ? S4 - nv : 0;
+    if (nv <= S4 && (ni == 0 || ni <= 4 * F)) {
+        if (s < nv) {
+            if (layer != 0) return 0;
+            first = 16 * s;
+            return 1;
+        }
+        const u64 j = layer * F + (s - nv);
+        if (j >= ni) return 0;
+        first = 16 * j;
+        return 2;
+    }
+    const u64 cv = nv / S4 + (s < nv % S4 ? 1u : 0u);
+    if (layer < cv) {
+        first = 16 * (layer * S4 + s);
+        return 1;
+    }
+    const u64 j = (layer - cv) * S4 + (S4 - 1 - s);
+    if (j >= ni) return 0;
+    first = 16 * j;
+    return 2;
+}
+
 template <int NL, int NR, int MODE_I, int MODE_V, bool QUAD = false>
 __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prove_prf_kernel(ProveArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
+    if constexpr (QUAD) {
+        if (A.place) {
+            u64 first = 0;
+            const int role = hb_prove_place(gridDim.x, blockIdx.x, threadIdx.x >> 6, A.n, !A.check_all, first);
+            if (role == 1) {
+                ProveVHandler<NL> hv{A};
+                hb_engine_quad<NL, NR, ProveVHandler<NL>>(hv, L, A.pv, A.n, A.queue + HB_QSLOT, A.qchunk, first);
+            } else if (role == 2) {
+                ProveIdxHandler<NL> hi{A};
+                hb_engine_quad<2, NR, ProveIdxHandler<NL>>(hi, L, A.pi, A.n, A.queue, A.qchunk, first);
+            }
+            return;
+        }
+    }
     // The two PRFs run side by side on disjoint halves of the grid: the
     // launch lasts as long as its longest rejection chain (a serial CFB
     // stream), and running the index chain before the v chain in the same

@@ -184,6 +184,7 @@ const SwitchName kSwitches[] = {
     {"HB_HOST_AHEAD", HB_SW_HOST_WINDOWS},
     {"HB_NO_PROVE_GATHER", HB_SW_NO_PROVE_GATHER},
     {"HB_SUMS_ON_DEVICE", HB_SW_SUMS_ON_DEVICE},
+    {"HB_NO_PROVE_PLACE", HB_SW_NO_PROVE_PLACE},
 };
 
 int nl_for_bits(int bits) {
@@ -1385,6 +1386,11 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     }
     // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
     const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
+    // quad engine: waves placed by SIMD, one v chain per SIMD where they fit
+    // (hb_prove_place; needs at most 16 waves per workgroup for the jobs);
+    // $HB_NO_PROVE_PLACE (test switch, A/B): waves race for the job queue
+    const u64 pwaves = 2 * ((n + 15) / 16);
+    PA.place = quad && pwaves <= 16ull * (u64)pgrid && !sw_env(c, "HB_NO_PROVE_PLACE") ? 1u : 0u;
     HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, quad ? 3 : mode_i, quad ? 3 : mode_v, pgrid, c->stream),
              "hb_prove_prf_kernel launch");
     c->last_launches++;
