@@ -156,7 +156,44 @@ struct ProveArgs {
     const unsigned char *tags;
     unsigned char *gdata;         // n x C
     unsigned char *gtags;         // n x tw
+    // Fused weighted sums (fuse != 0, hb_prove_fused): the index waves gather
+    // their blocks into the workgroup's LDS arena, summer waves of the same
+    // workgroup add the terms as their index and v arrive, and the last
+    // workgroup finishes the sums -- no hb_wsum_kernel launch.
+    u32 fuse;
+    u32 ncols;                    // S + 1
+    u32 fcmax;                    // most jobs of one workgroup (<= HB_FZ_MAXJOBS)
+    u32 fsec16, ftag16;           // sectors / tags load as 16-byte words (ss == 4 NL / tw == 4 NL)
+    u32 ftoken;                   // completion token (never 0), as hb_wsum_kernel's
+    unsigned long long *facc;     // [ncols][NL] limb sums over workgroups, zero between launches
+    unsigned int *fctl;           // finished-workgroup counter, zero between launches
+    u32 *fout;                    // [ncols][NL] results, the status word, the token word
 };
+
+// The fused prove's LDS arena (next to the 128 KiB T-table image): byte
+// offsets of [0] the per-job index / v ready flags (2 cmax words) and 4
+// counters, [1] the v slots (cmax x NL words), [2] the workgroup's limb sums
+// (ncols x NL u64), [3] the gathered blocks (cmax x C bytes), [4] their tags
+// (cmax x tw); returns the arena's size.
+#define HB_FZ_BYTES 30720
+#define HB_FZ_MAXJOBS 48
+HB_HHD u64 hb_fz_layout(u32 cmax, u32 nl, u32 ncols, u64 C, u32 tw, u32 off[5]) {
+    u64 o = (2ull * cmax + 4) * 4;
+    off[0] = 0;
+    o = (o + 15) & ~15ull;
+    off[1] = (u32)o;
+    o += (u64)cmax * nl * 4;
+    o = (o + 15) & ~15ull;
+    off[2] = (u32)o;
+    o += (u64)ncols * nl * 8;
+    o = (o + 15) & ~15ull;
+    off[3] = (u32)(o < 0xffffffffull ? o : 0);
+    o += (u64)cmax * C;
+    o = (o + 15) & ~15ull;
+    off[4] = (u32)(o < 0xffffffffull ? o : 0);
+    o += (u64)cmax * tw;
+    return o;
+}
 
 // Weighted sums  sum_i w_i * value_{col}(i)  mod p  (w_i in Montgomery form);
 // modes: see hb_wsum_kernel.

@@ -309,11 +309,14 @@ __device__ __forceinline__ u32 hb_quad_prf_try(const QuadLane &Q, const u32 *rkq
 // hb_engine (MODE 0, fresh evaluations: h.init zeroes the register) with one
 // job per quad.  Only lane q = 0 of a quad takes jobs and calls h.accept; the
 // job index is broadcast to the quad.  `chunk` = jobs per refill per wave
-// (16 = one per quad).  `first` != ~0: the wave runs jobs [first, first + 16)
-// and never touches the queue (placed waves, hb_prove_place).
+// (16 = one per quad).  `first` != ~0: the wave runs jobs [first, min(first
+// + 16, njobs, end)) and never touches the queue (placed waves,
+// hb_prove_place).  A job abandoned after HB_MAX_TRIES is reported to
+// h.fail (the fused prove's consumers wait for every job).
 template <int NL, int NR, class H>
 __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const PrfParams<NL> &P, u64 njobs,
-                                               unsigned long long *queue, u64 chunk, u64 first = ~0ull) {
+                                               unsigned long long *queue, u64 chunk, u64 first = ~0ull,
+                                               u64 end = ~0ull) {
     const QuadLane Q = hb_quad_lane(L);
     const u32 q = hb_lane_id() & 3u;
     const bool lead = q == 0;
@@ -327,8 +330,10 @@ __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const Prf
         const u32 k2 = __builtin_amdgcn_readfirstlane(P.rk[4 * r + 2]), k3 = __builtin_amdgcn_readfirstlane(P.rk[4 * r + 3]);
         rkq[r] = q == 0 ? k0 : q == 1 ? k1 : q == 2 ? k2 : k3;
     }
+    u64 stop = njobs - first < 16 ? njobs : first + 16;
+    if (stop > end) stop = end;
     HbPool pool = first == ~0ull ? HbPool{0, 0, njobs, queue, false, chunk}
-                                 : HbPool{first, njobs - first < 16 ? njobs : first + 16, njobs, queue, true, chunk};
+                                 : HbPool{first, stop, njobs, queue, true, chunk};
     u64 job = 0;
     bool active = pool.take(__ballot(lead), lead, job);
     job = hb_qbcast64(job);
@@ -344,6 +349,7 @@ __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const Prf
         if (acc && lead) h.accept(job, out);
         const bool give_up = active && !ok && job_tries >= HB_MAX_TRIES;
         failed += give_up && lead ? 1u : 0u;
+        if (give_up && lead) h.fail(job);
         const bool next = acc || give_up;
         const u64 m = __ballot(next && lead);
         if (m) {
@@ -1033,6 +1039,7 @@ struct PrfHandler {
         return true;
     }
     __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void fail(u64) const {}
     __device__ __forceinline__ void accept(u64 job, const u32 v[NL]) const {
         u32 *o = A.out + job * NL;
         for (int t = 0; t < NL; ++t) o[t] = v[t];
@@ -1074,11 +1081,9 @@ __global__ __launch_bounds__(256) void hb_mont_kernel(MontArgs<NL> A) {
 // job of the compact gather buffers: the device twin of the host gather
 // (hb_runtime.cpp, Gather::run).  One lane; whole-block 16-byte copies when
 // the block lies inside the file and everything is 16-byte aligned.
-__device__ __forceinline__ void hb_gather_block(const unsigned char *data, u64 len, u64 C, u32 ss, u32 S,
-                                                const unsigned char *tags, u32 tw, u64 ntags, u32 align16,
-                                                unsigned char *gdata, unsigned char *gtags, u64 job, u64 ix) {
-    unsigned char *dst = gdata + job * C;
-    unsigned char *tdst = gtags + job * (u64)tw;
+__device__ __forceinline__ void hb_gather_to(const unsigned char *data, u64 len, u64 C, u32 ss, u32 S,
+                                             const unsigned char *tags, u32 tw, u64 ntags, u32 align16,
+                                             unsigned char *dst, unsigned char *tdst, u64 ix) {
     if (ix >= ntags) {   // reported by the host (flags); summed as 0
         for (u64 b = 0; b < C; ++b) dst[b] = 0;
         for (u32 b = 0; b < tw; ++b) tdst[b] = 0;
@@ -1090,15 +1095,20 @@ __device__ __forceinline__ void hb_gather_block(const unsigned char *data, u64 l
         const uint4 *s = reinterpret_cast<const uint4 *>(data + base);
         uint4 *d = reinterpret_cast<uint4 *>(dst);
         const u64 nq = C / 16;
-        for (u64 k = 0; k < nq; k += 8) {
-            uint4 v[8];
-            HB_UNROLL
-            for (int j = 0; j < 8; ++j)
-                if (k + j < nq) v[j] = s[k + j];
-            HB_UNROLL
-            for (int j = 0; j < 8; ++j)
-                if (k + j < nq) d[k + j] = v[j];
+        u64 k = 0;
+        for (; k + 8 <= nq; k += 8) {   // (named values: an array of them was kept in scratch)
+            const uint4 v0 = s[k], v1 = s[k + 1], v2 = s[k + 2], v3 = s[k + 3];
+            const uint4 v4 = s[k + 4], v5 = s[k + 5], v6 = s[k + 6], v7 = s[k + 7];
+            d[k] = v0;
+            d[k + 1] = v1;
+            d[k + 2] = v2;
+            d[k + 3] = v3;
+            d[k + 4] = v4;
+            d[k + 5] = v5;
+            d[k + 6] = v6;
+            d[k + 7] = v7;
         }
+        for (; k < nq; ++k) d[k] = s[k];
     } else {
         for (u32 j = 0; j < S; ++j) {
             const u64 pos = base + (u64)j * ss;
@@ -1117,11 +1127,18 @@ __device__ __forceinline__ void hb_gather_block(const unsigned char *data, u64 l
     }
 }
 
+__device__ __forceinline__ void hb_gather_block(const unsigned char *data, u64 len, u64 C, u32 ss, u32 S,
+                                                const unsigned char *tags, u32 tw, u64 ntags, u32 align16,
+                                                unsigned char *gdata, unsigned char *gtags, u64 job, u64 ix) {
+    hb_gather_to(data, len, C, ss, S, tags, tw, ntags, align16, gdata + job * C, gtags + job * (u64)tw, ix);
+}
+
 template <int NL>
 struct ProveIdxHandler {
     const ProveArgs<NL> &A;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.i0 + job; }
     __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void fail(u64) const {}
     __device__ __forceinline__ void accept(u64 job, const u32 v[2]) const {
         const u64 ix = (u64)v[0] | ((u64)v[1] << 32);
         A.idx[job] = ix;
@@ -1141,6 +1158,7 @@ struct ProveVHandler {
     const ProveArgs<NL> &A;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.i0 + job; }
     __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void fail(u64) const {}
     __device__ __forceinline__ void accept(u64 job, const u32 v[NL]) const {
         u32 y[NL];
         hb_to_mont<NL>(v, A.r2, A.mod, y);
@@ -1190,9 +1208,257 @@ __device__ __forceinline__ int hb_prove_place(u32 G, u32 g, u32 w, u64 n, bool i
     return 2;
 }
 
+// ------------------------------------------------------------------ fused prove
+// One launch for the whole PySwizzle prove of a device-resident file when
+// everything fits one workgroup's LDS (hb_runtime.cpp decides, A.fuse):
+// workgroup g owns jobs [j0, j1) = [n g / G, n (g + 1) / G) (<= 48), and its
+// 16 waves split as
+//   waves 0-2    v waves (16 jobs each), one per SIMD (hb_prove_place's HW_ID
+//                order: waves 4m .. 4m+3 sit on the CU's four SIMDs)
+//   waves 3,7,11 index waves, stacked on the fourth SIMD (their chains are
+//                ~1/3 of a v chain: 4 CFB-8 steps per try against 32)
+//   waves 12-15  summers, one per SIMD (their work is ~1 % of a SIMD's issue)
+//   the rest     exit after the table fill.
+// An index wave gathers job k's block and tag from HBM into LDS slot k (the
+// host gather's layout) and raises iflag[k]; a v wave stores v_k R mod p in
+// LDS and raises vflag[k] (workgroup-scope release / acquire).  Summer lane
+// l owns column l mod ncols and jobs k = l / ncols + r * (256 / ncols): it
+// polls its jobs' flags and multiply-accumulates each term as soon as both
+// halves are there, so the sums ride under the v chains instead of following
+// them in a second launch (hb_wsum_kernel, ~26 us at configs[4]).  Then the
+// summers' residues go into per-column u64 limb sums in LDS (ds_add_u64),
+// summer wave 12 -- once every producer wave and summer wave has signalled --
+// adds the workgroup's limb sums into the global ones (agent-scope atomics),
+// and the last workgroup to finish (agent counter) carries, reduces and
+// writes the ncols results, the status word and the completion token into
+// the pinned host buffer, re-zeroing the limb sums, the counter, the PRF
+// slots and the flag word -- the invariants of hb_wsum_kernel (I1-I4) hold
+// for fctl / facc as for ctl.  Nobody waits on anything but producers of its
+// own workgroup, which never wait: no co-residency assumption across
+// workgroups.  Every job raises its flags, abandoned ones too (h.fail); the
+// waits are bounded anyway (HB_FUSE_SPINS polls, ~0.4 s), and a timeout
+// raises flag bit 2 -> status bit 4 -> a loud error on the host.
+#ifndef HB_FUSE_SPINS
+#define HB_FUSE_SPINS (1u << 22)
+#endif
+
+struct HbFz {
+    u32 *iflag, *vflag, *ctr;     // ctr[0] producer waves done, [1] summer waves done, [2] timeout
+    u32 *v;
+    unsigned long long *acc;
+    unsigned char *blk, *tag;
+};
+
+template <int NL>
+__device__ __forceinline__ HbFz hb_fz(unsigned char *base, const ProveArgs<NL> &A) {
+    u32 off[5];
+    hb_fz_layout(A.fcmax, NL, A.ncols, A.C, A.tw, off);
+    HbFz z;
+    z.iflag = (u32 *)base;
+    z.vflag = z.iflag + A.fcmax;
+    z.ctr = z.vflag + A.fcmax;
+    z.v = (u32 *)(base + off[1]);
+    z.acc = (unsigned long long *)(base + off[2]);
+    z.blk = base + off[3];
+    z.tag = base + off[4];
+    return z;
+}
+
+__device__ __forceinline__ void hb_fz_raise(u32 *flag) {
+    __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ u32 hb_fz_get(const u32 *flag) {
+    return __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int NL>
+struct FusedIdxHandler {
+    const ProveArgs<NL> &A;
+    const HbFz &z;
+    u64 j0;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return A.i0 + job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void gather(u64 job, u64 ix) const {
+        const u64 k = job - j0;
+        hb_gather_to(A.data, A.len, A.C, A.ss, A.S, A.tags, A.tw, A.ntags, A.galign16, z.blk + k * A.C,
+                     z.tag + k * (u64)A.tw, ix);
+        hb_fz_raise(z.iflag + k);
+    }
+    __device__ __forceinline__ void accept(u64 job, const u32 v[2]) const {
+        const u64 ix = (u64)v[0] | ((u64)v[1] << 32);
+        if (ix >= A.ntags) atomicOr(A.flags, 1u);   // as ProveIdxHandler; summed as 0
+        gather(job, ix);
+    }
+    __device__ __forceinline__ void fail(u64 job) const { gather(job, A.ntags); }   // zeros; status bit 2
+};
+
+template <int NL>
+struct FusedVHandler {
+    const ProveArgs<NL> &A;
+    const HbFz &z;
+    u64 j0;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return A.i0 + job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void accept(u64 job, const u32 v[NL]) const {
+        u32 y[NL];
+        hb_to_mont<NL>(v, A.r2, A.mod, y);
+        u32 *o = z.v + (job - j0) * NL;
+        for (int t = 0; t < NL; ++t) o[t] = y[t];
+        hb_fz_raise(z.vflag + (job - j0));
+    }
+    __device__ __forceinline__ void fail(u64 job) const {
+        u32 *o = z.v + (job - j0) * NL;
+        for (int t = 0; t < NL; ++t) o[t] = 0;
+        hb_fz_raise(z.vflag + (job - j0));
+    }
+};
+
+// Summer wave (12 .. 15) of the fused prove.
+template <int NL>
+__device__ __forceinline__ void hb_fused_sum(const ProveArgs<NL> &A, const HbFz &z, u64 j0, u64 j1) {
+    const u32 l = threadIdx.x - 12u * 64u, nc = A.ncols, R = 256u / nc;
+    const u32 col = l % nc, r = l / nc, cnt = (u32)(j1 - j0);
+    bool timeout = false;
+    if (r < R) {
+        u32 acc[2 * NL + 1];
+        for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
+        u64 pending = 0;
+        for (u32 k = r; k < cnt; k += R) pending |= 1ull << k;
+        u32 spins = 0;
+        while (pending) {
+            u64 pm = pending;
+            bool any = false;
+            while (pm) {
+                const u32 k = (u32)__builtin_ctzll(pm);
+                pm &= pm - 1;
+                if (!hb_fz_get(z.vflag + k) || !hb_fz_get(z.iflag + k)) continue;
+                u32 m[NL];
+                if (col < A.S) {
+                    const u64 off = (u64)k * A.C + (u64)col * A.ss;
+                    if (A.fsec16) hb_load_full16<NL>(z.blk, off, m);
+                    else hb_load_be_bytes<NL>(z.blk, off, A.ss, m);
+                } else {
+                    if (A.ftag16) hb_load_full16<NL>(z.tag, (u64)k * A.tw, m);
+                    else hb_load_be_bytes<NL>(z.tag, (u64)k * A.tw, A.tw, m);
+                }
+                hb_mac<NL>(acc, z.v + (u64)k * NL, m);
+                pending &= ~(1ull << k);
+                any = true;
+            }
+            if (!any) {
+                if (++spins > HB_FUSE_SPINS) {
+                    timeout = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        u32 v[NL + 1], res[NL];
+        hb_redc<NL>(acc, A.mod, v);
+        hb_reduce_small<NL>(v, A.mod, res);
+        for (int t = 0; t < NL; ++t)
+            __hip_atomic_fetch_add(z.acc + col * NL + t, (unsigned long long)res[t], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (__ballot(timeout)) {
+        if (hb_lane_id() == 0) __hip_atomic_store(z.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (hb_lane_id() == 0) __hip_atomic_fetch_add(z.ctr + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (threadIdx.x >> 6 != 12) return;
+    // wave 12: every summer and producer wave of this workgroup has signalled
+    u32 spins = 0;
+    while (__hip_atomic_load(z.ctr + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u ||
+           __hip_atomic_load(z.ctr + 0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 6u) {
+        if (++spins > HB_FUSE_SPINS) {
+            timeout = true;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    for (u32 i = hb_lane_id(); i < nc * NL; i += 64) {
+        const unsigned long long x = __hip_atomic_load(z.acc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (x) __hip_atomic_fetch_add(A.facc + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const bool to = __ballot(timeout) != 0 || __hip_atomic_load(z.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (to && hb_lane_id() == 0) atomicOr(A.flags, 4u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    u32 lastw = 0;
+    if (hb_lane_id() == 0)
+        lastw = __hip_atomic_fetch_add(A.fctl, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x;
+    if (!__builtin_amdgcn_readfirstlane(lastw)) return;
+    // the last workgroup: carry, reduce and write the ncols sums, re-zero
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (u32 c = hb_lane_id(); c < nc; c += 64) {
+        u32 v[NL + 1], o[NL];
+        u64 carry = 0;
+        for (int t = 0; t < NL; ++t) {
+            unsigned long long *a = A.facc + c * NL + t;
+            carry += __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[t] = (u32)carry;
+            carry >>= 32;
+        }
+        v[NL] = (u32)carry;      // < 2^16 p in all: 255 residues < p per workgroup
+        hb_reduce_small<NL>(v, A.mod, o);
+        for (int t = 0; t < NL; ++t) A.fout[(u64)c * NL + t] = o[t];
+    }
+    if (hb_lane_id() == 0) {
+        u32 st = 0;
+        for (u32 q = 0; q < 2; ++q) {
+            unsigned long long *qs = A.queue + (u64)q * HB_QSLOT;
+            st |= __hip_atomic_load(qs + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 2u : 0u;
+            for (int k2 = 0; k2 < HB_QSLOT; ++k2) __hip_atomic_store(qs + k2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const u32 fl = __hip_atomic_load(A.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st |= (fl & 1u) | ((fl & 4u) ? 4u : 0u);
+        __hip_atomic_store(A.flags, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(A.fctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        A.fout[(u64)nc * NL] = st;
+        A.fout[(u64)nc * NL + 1] = A.ftoken;
+    }
+}
+
+template <int NL, int NR>
+__device__ __forceinline__ void hb_prove_fused(const ProveArgs<NL> &A, const LaneTab &L, const HbFz &z) {
+    const u64 G = gridDim.x, g = blockIdx.x;
+    const u64 j0 = A.n * g / G, j1 = A.n * (g + 1) / G;
+    const u32 w = threadIdx.x >> 6;
+    if (w < 4 || w == 7 || w == 11) {
+        const bool isv = w < 3;
+        const u64 first = j0 + 16ull * (isv ? w : w >> 2);
+        if (first < j1) {
+            if (isv) {
+                FusedVHandler<NL> h{A, z, j0};
+                hb_engine_quad<NL, NR, FusedVHandler<NL>>(h, L, A.pv, A.n, A.queue + HB_QSLOT, A.qchunk, first, j1);
+            } else {
+                FusedIdxHandler<NL> h{A, z, j0};
+                hb_engine_quad<2, NR, FusedIdxHandler<NL>>(h, L, A.pi, A.n, A.queue, A.qchunk, first, j1);
+            }
+        }
+        // the engine's statistics (q[1], q[2]) before the signal
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (hb_lane_id() == 0) __hip_atomic_fetch_add(z.ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (w >= 12) {
+        hb_fused_sum<NL>(A, z, j0, j1);
+    }
+}
+
 template <int NL, int NR, int MODE_I, int MODE_V, bool QUAD = false>
 __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prove_prf_kernel(ProveArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    if constexpr (QUAD) {
+        if (A.fuse) {
+            __shared__ __attribute__((aligned(16))) unsigned char fz[HB_FZ_BYTES];
+            const HbFz z = hb_fz<NL>(fz, A);
+            // flags, counters and limb sums start at zero (ordered by the fill's barrier)
+            for (u32 i = threadIdx.x; i < 2 * A.fcmax + 4; i += blockDim.x) z.iflag[i] = 0;
+            for (u32 i = threadIdx.x; i < A.ncols * NL; i += blockDim.x) z.acc[i] = 0;
+            hb_fill_lds(lds, A.t0);
+            hb_prove_fused<NL, NR>(A, hb_lane_tab(lds), z);
+            return;
+        }
+    }
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     if constexpr (QUAD) {

@@ -99,6 +99,7 @@ struct hb_ctx {
     DevBuf ctl;          // wsum column counters + flags (zero between operations)
     DevBuf mseeds, moffs, mdig;   // Merkle chunk seeds, offsets, HMAC digests
     DevBuf gdev;         // device-resident prove: the challenged blocks and tags, gathered
+    DevBuf facc;         // fused prove: per-column limb sums over workgroups (zero between operations)
     HostBuf gstage[2];   // host-file prove: pinned gather buffers (blocks | tags), double-buffered
     HostBuf hscratch;    // pinned staging of the encode's small host round trips (alpha, MFMA tables)
     // the alpha D2H into hscratch done / the MFMA-table H2D out of it done
@@ -185,6 +186,7 @@ const SwitchName kSwitches[] = {
     {"HB_NO_PROVE_GATHER", HB_SW_NO_PROVE_GATHER},
     {"HB_SUMS_ON_DEVICE", HB_SW_SUMS_ON_DEVICE},
     {"HB_NO_PROVE_PLACE", HB_SW_NO_PROVE_PLACE},
+    {"HB_NO_PROVE_FUSE", HB_SW_NO_PROVE_FUSE},
 };
 
 int nl_for_bits(int bits) {
@@ -1311,6 +1313,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         HB_CHECK(hipMemsetAsync(c->queue + HB_QSLOT * 2, 0, 2 * HB_QSLOT * sizeof(unsigned long long), c->stream),
                  "hipMemsetAsync");
         if (c->ctl.n) HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync");
+        if (c->facc.n) HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync");
         c->prove_dirty = false;
         c->ctl_dirty = false;
     }
@@ -1371,7 +1374,52 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     const bool galign16 = (uintptr_t)data % 16 == 0 && (uintptr_t)tags % 16 == 0 && C % 16 == 0 && pi.tw % 16 == 0;
     const bool dev_gather = data_dev && tags_dev && !cxx && !check_all && galign16 &&
                             !sw_env(c, "HB_NO_PROVE_GATHER") && n * (C + pi.tw) <= (64ull << 20);
-    if (dev_gather) {
+    // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
+    const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
+    // quad engine: waves placed by SIMD, one v chain per SIMD where they fit
+    // (hb_prove_place; needs at most 16 waves per workgroup for the jobs);
+    // $HB_NO_PROVE_PLACE (test switch, A/B): waves race for the job queue
+    const u64 pwaves = 2 * ((n + 15) / 16);
+    PA.place = quad && pwaves <= 16ull * (u64)pgrid && !sw_env(c, "HB_NO_PROVE_PLACE") ? 1u : 0u;
+    // Fused weighted sums (hb_prove_fused): placed quad waves, a device
+    // gather, at most 48 jobs per workgroup whose blocks, tags and sums fit
+    // the LDS arena, primes up to 512 bits (the summers' registers);
+    // $HB_NO_PROVE_FUSE (test switch, A/B): the PRF launch + hb_wsum_kernel
+    const u64 fcmax = (n + (u64)pgrid - 1) / (u64)pgrid;
+    u32 fzoff[5];
+    const bool fuse = dev_gather && PA.place && NL <= 16 && ncols <= 256 && fcmax <= HB_FZ_MAXJOBS &&
+                      hb_fz_layout((u32)fcmax, NL, ncols, C, pi.tw, fzoff) <= HB_FZ_BYTES &&
+                      !sw_env(c, "HB_NO_PROVE_FUSE");
+    if (fuse) {
+        const void *was = c->facc.p;
+        HB_CHECK(c->facc.ensure((size_t)ncols * NL * 8), "hipMalloc(facc)");
+        if (c->facc.p != was) HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync(facc)");
+        if (c->ctl_dirty) {
+            HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync(ctl)");
+            HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync(facc)");
+            c->ctl_dirty = false;
+        }
+        const size_t words = (size_t)ncols * NL + 2;
+        if (int rc = ensure_hres(c, words)) return rc;
+        c->sums_in_hres = true;
+        PA.fuse = 1u;
+        PA.ncols = ncols;
+        PA.fcmax = (u32)fcmax;
+        PA.fsec16 = pi.ss == 4u * NL && pi.ss % 16 == 0 ? 1u : 0u;
+        PA.ftag16 = pi.tw == 4u * NL ? 1u : 0u;
+        PA.ftoken = next_token(c, true);
+        PA.facc = (unsigned long long *)c->facc.p;
+        PA.fctl = (unsigned int *)c->ctl.p;
+        PA.fout = c->hres;
+        PA.data = data;
+        PA.len = len;
+        PA.C = C;
+        PA.ss = pi.ss;
+        PA.S = S;
+        PA.tw = pi.tw;
+        PA.tags = tags;
+        PA.galign16 = 1u;
+    } else if (dev_gather) {
         HB_CHECK(c->gdev.ensure((size_t)(gstride + n * pi.tw)), "hipMalloc(gather)");
         PA.data = data;
         PA.len = len;
@@ -1384,13 +1432,6 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         PA.gtags = (unsigned char *)c->gdev.p + gstride;
         PA.galign16 = 1u;
     }
-    // the index and v PRFs on disjoint halves of the grid (hb_prove_prf_kernel)
-    const int pgrid = !check_all && es.grid < 2 ? 2 : es.grid;
-    // quad engine: waves placed by SIMD, one v chain per SIMD where they fit
-    // (hb_prove_place; needs at most 16 waves per workgroup for the jobs);
-    // $HB_NO_PROVE_PLACE (test switch, A/B): waves race for the job queue
-    const u64 pwaves = 2 * ((n + 15) / 16);
-    PA.place = quad && pwaves <= 16ull * (u64)pgrid && !sw_env(c, "HB_NO_PROVE_PLACE") ? 1u : 0u;
     HB_CHECK(hb_launch_prove_prf<NL>(PA, nr, quad ? 3 : mode_i, quad ? 3 : mode_v, pgrid, c->stream),
              "hb_prove_prf_kernel launch");
     c->last_launches++;
@@ -1409,7 +1450,9 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     A.qslots = PA.queue;
     A.nslots = 2;
     int rc = 0;
-    if (dev_gather) {
+    if (fuse) {
+        // the sums were taken inside the PRF launch
+    } else if (dev_gather) {
         A.mode = 2;
         A.w = (const u32 *)c->wts.p;
         A.nterms = n;
@@ -1682,7 +1725,8 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->copy) (void)hipStreamSynchronize(c->copy);
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
                       &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
-                      &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig, &c->gdev};
+                      &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig, &c->gdev,
+                      &c->facc};
     for (DevBuf *b : bufs) b->release();
     if (c->hres) (void)hipHostFree(c->hres);
     c->gstage[0].release();

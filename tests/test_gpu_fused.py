@@ -1,0 +1,161 @@
+"""The fused device prove (round 5, hb_kernels.hpp hb_prove_fused): one launch
+in which each workgroup's index waves gather their challenged blocks into LDS,
+its v waves store v R mod p there, and summer waves add the terms as both
+halves arrive; the last workgroup finishes the sums.  Every case is proved
+twice on one context -- fused, and with HB_NO_PROVE_FUSE (PRF launch +
+hb_wsum_kernel) -- and both must equal the oracle.  The launch count tells
+which path ran (1 = fused): the cases cover the shapes the host admits (48
+jobs per workgroup and one more, NL = 8 and 16, 16-byte and byte-wise sector
+and tag loads, 2 to 65 columns, empty and ragged files, repeated proves on
+one context: the limb sums and counters re-zeroed by each launch's closer).
+
+Bar: bit-exact.  Reference: PySwizzle.py:333-370 (prove)."""
+import ctypes
+import hashlib
+import importlib
+import random
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _prime(bits):
+    if bits == 256:
+        return int(load_golden("primes.json")["p256"], 16)
+    pys = importlib.import_module("heartbeat_amd.PySwizzle.PySwizzle")
+    rng = random.Random(7000 + bits)
+    while True:
+        x = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        if pys._is_probable_prime(x):
+            return x
+
+
+def _ints(raw, w, n):
+    return [int.from_bytes(raw[j * w:(j + 1) * w], "big") for j in range(n)]
+
+
+# (prime bits, sectors, file bytes, challenge chunks, fused?)
+CASES = [
+    (256, 16, (16 << 20) + 77, 10000, True),     # configs[4]'s shape at 16 MiB, ragged tail block
+    (256, 16, 8 << 20, 12288, True),             # 48 jobs in every workgroup (256 of them)
+    (256, 16, 8 << 20, 12289, False),            # one more: the two-launch sum
+    (256, 1, (1 << 20) + 5, 3000, True),         # two columns
+    (256, 16, 0, 5, True),                       # empty file: every sector past EOF
+    (256, 64, 1 << 20, 300, True),               # 65 columns, 3 summer lanes each
+    (512, 3, 300000, 4000, True),                # NL = 16, 16-byte sector loads
+    (384, 7, 250000, 2500, True),                # NL = 16, 48-byte sectors: byte-wise loads
+    (128, 16, 100000, 1000, True),               # NL = 8, 16-byte sectors and tags: byte-wise loads
+]
+
+
+def test_fused_prove_equals_two_launch_sum_and_oracle(oracle, monkeypatch):
+    from heartbeat_amd import _native as nat
+    ctx = nat.context()
+    L = nat.lib()
+    rng = np.random.default_rng(55)
+    for k, (bits, S, n, chunks, fused) in enumerate(CASES):
+        p = _prime(bits)
+        w = nat.width_of(p)
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        fk, ak = hashlib.sha256(b"fz-f%d" % k).digest(), hashlib.sha256(b"fz-a%d" % k).digest()
+        tags = oracle.encode(p, S, fk, ak, data, nthreads=8)
+        nb = len(tags)
+        traw = np.frombuffer(b"".join(t.to_bytes(w, "big") for t in tags), dtype=np.uint8)
+        dd, dt = ctypes.c_void_p(), ctypes.c_void_p()
+        ctx.check(L.hb_device_malloc(ctx.h, max(n, 16), ctypes.byref(dd)))
+        ctx.check(L.hb_device_malloc(ctx.h, len(traw), ctypes.byref(dt)))
+        try:
+            if n:
+                hd = np.frombuffer(data, dtype=np.uint8)
+                ctx.check(L.hb_memcpy(ctx.h, dd, hd.ctypes.data, n, 1))
+            ctx.check(L.hb_memcpy(ctx.h, dt, traw.ctypes.data, len(traw), 1))
+            pb = nat.be(p)
+            want = oracle.prove(p, S, hashlib.sha256(b"fz-c%d" % k).digest(), chunks, p, tags, data)
+            for off in (False, True, False):
+                if off:
+                    monkeypatch.setenv("HB_NO_PROVE_FUSE", "1")
+                else:
+                    monkeypatch.delenv("HB_NO_PROVE_FUSE", raising=False)
+                key = hashlib.sha256(b"fz-c%d" % k).digest()
+                mu = ctypes.create_string_buffer(w * S)
+                sg = ctypes.create_string_buffer(w)
+                ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, key, 32, chunks, pb, len(pb), dt, nb, dd, n, 3, mu, sg))
+                ms, nl = ctypes.c_double(), ctypes.c_uint32()
+                ctx.check(L.hb_last_kernel_ms(ctx.h, ctypes.byref(ms), ctypes.byref(nl)))
+                assert nl.value == (1 if fused and not off else 2), (bits, S, n, chunks, off, nl.value)
+                got = (_ints(mu.raw, w, S), int.from_bytes(sg.raw, "big"))
+                assert got == want, (bits, S, n, chunks, "two-launch" if off else "fused")
+        finally:
+            monkeypatch.delenv("HB_NO_PROVE_FUSE", raising=False)
+            ctx.check(L.hb_device_free(ctx.h, dd))
+            ctx.check(L.hb_device_free(ctx.h, dt))
+
+
+def test_fused_prove_ranges_sum_to_whole(oracle):
+    """hb_prove_range halves (the multi-GPU split of a challenge) each run
+    fused and add up mod p to the whole proof (PySwizzle.py:351-368)."""
+    from heartbeat_amd import _native as nat
+    ctx = nat.context()
+    L = nat.lib()
+    p = _prime(256)
+    w = nat.width_of(p)
+    S, n, chunks = 16, 4 << 20, 10000
+    data = np.random.default_rng(9).integers(0, 256, n, dtype=np.uint8).tobytes()
+    tags = oracle.encode(p, S, b"r" * 32, b"s" * 32, data, nthreads=8)
+    traw = np.frombuffer(b"".join(t.to_bytes(w, "big") for t in tags), dtype=np.uint8)
+    dd, dt = ctypes.c_void_p(), ctypes.c_void_p()
+    ctx.check(L.hb_device_malloc(ctx.h, n, ctypes.byref(dd)))
+    ctx.check(L.hb_device_malloc(ctx.h, len(traw), ctypes.byref(dt)))
+    try:
+        ctx.check(L.hb_memcpy(ctx.h, dd, np.frombuffer(data, dtype=np.uint8).ctypes.data, n, 1))
+        ctx.check(L.hb_memcpy(ctx.h, dt, traw.ctypes.data, len(traw), 1))
+        pb, key = nat.be(p), hashlib.sha256(b"halves").digest()
+        parts = []
+        for i0, i1 in ((0, 4321), (4321, chunks)):
+            mu = ctypes.create_string_buffer(w * S)
+            sg = ctypes.create_string_buffer(w)
+            ctx.check(L.hb_prove_range(ctx.h, pb, len(pb), S, key, 32, chunks, i0, i1, pb, len(pb), dt, len(tags),
+                                       dd, n, 3, mu, sg))
+            parts.append((_ints(mu.raw, w, S), int.from_bytes(sg.raw, "big")))
+        mu = [(a + b) % p for a, b in zip(parts[0][0], parts[1][0])]
+        assert (mu, (parts[0][1] + parts[1][1]) % p) == oracle.prove(p, S, key, chunks, p, tags, data)
+    finally:
+        ctx.check(L.hb_device_free(ctx.h, dd))
+        ctx.check(L.hb_device_free(ctx.h, dt))
+
+
+def test_unplaced_queue_engine_prove_equals_oracle(oracle, monkeypatch):
+    """With HB_NO_PROVE_PLACE the PRF waves race for the job queue (the
+    pre-placement engine) and the sum takes its own launch: same proof."""
+    from heartbeat_amd import _native as nat
+    ctx = nat.context()
+    L = nat.lib()
+    p = _prime(256)
+    w = nat.width_of(p)
+    S, n, chunks = 16, 2 << 20, 10000
+    data = np.random.default_rng(10).integers(0, 256, n, dtype=np.uint8).tobytes()
+    tags = oracle.encode(p, S, b"q" * 32, b"u" * 32, data, nthreads=8)
+    traw = np.frombuffer(b"".join(t.to_bytes(w, "big") for t in tags), dtype=np.uint8)
+    dd, dt = ctypes.c_void_p(), ctypes.c_void_p()
+    ctx.check(L.hb_device_malloc(ctx.h, n, ctypes.byref(dd)))
+    ctx.check(L.hb_device_malloc(ctx.h, len(traw), ctypes.byref(dt)))
+    monkeypatch.setenv("HB_NO_PROVE_PLACE", "1")
+    try:
+        ctx.check(L.hb_memcpy(ctx.h, dd, np.frombuffer(data, dtype=np.uint8).ctypes.data, n, 1))
+        ctx.check(L.hb_memcpy(ctx.h, dt, traw.ctypes.data, len(traw), 1))
+        pb, key = nat.be(p), hashlib.sha256(b"queue").digest()
+        mu = ctypes.create_string_buffer(w * S)
+        sg = ctypes.create_string_buffer(w)
+        ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, key, 32, chunks, pb, len(pb), dt, len(tags), dd, n, 3, mu, sg))
+        ms, nl = ctypes.c_double(), ctypes.c_uint32()
+        ctx.check(L.hb_last_kernel_ms(ctx.h, ctypes.byref(ms), ctypes.byref(nl)))
+        assert nl.value == 2
+        assert (_ints(mu.raw, w, S), int.from_bytes(sg.raw, "big")) == oracle.prove(p, S, key, chunks, p, tags, data)
+    finally:
+        monkeypatch.delenv("HB_NO_PROVE_PLACE", raising=False)
+        ctx.check(L.hb_device_free(ctx.h, dd))
+        ctx.check(L.hb_device_free(ctx.h, dt))
