@@ -107,6 +107,9 @@ def parse(argv=None):
                          "for the N = 1 configs[2] run)")
     ap.add_argument("--host-path", action="store_true",
                     help="time the host-memory path rows in any configuration")
+    ap.add_argument("--no-prove", action="store_true",
+                    help="skip the configs[4] prove row of the default N = 1 configs[2] run")
+    ap.add_argument("--prove-proofs", type=int, default=200, help="timed proofs of that row")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the launch / rank / timing / JSON plumbing without HIP calls (CPU tests)")
     args = ap.parse_args(argv)
@@ -466,6 +469,13 @@ def bench_encode(args, cfg, R):
 
     if args.sustain_seconds > 0 and len(pieces) == 1:
         line["sustained"] = sustained(args, R, step, elapsed / args.steps, file_len)
+    # configs[4] on this very file (64 GiB, S = 16, 256-bit prime, its tags
+    # just computed): the prove row of the same run, before the host-path rows
+    # reuse the device buffer
+    if R.rank == 0 and R.world == 1 and args.config == "c3" and not cxx and not args.no_prove and len(pieces) == 1:
+        t = time.perf_counter()
+        line["prove"] = prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, proofs=args.prove_proofs)
+        line["prove"]["seconds_spent"] = round(time.perf_counter() - t, 1)
     # the host-memory rows come right after the device-resident ones: after
     # the CPU rows (16 threads streaming 64 GiB through host buffers) the same
     # rows measured 21-25 instead of 31-38 GiB/s for a real file
@@ -879,6 +889,80 @@ def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
     out["api_tags_equal"] = api_ok
     out["unit"] = "GiB/s"
     return out
+
+
+def prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, proofs=200, chunks=10000):
+    """configs[4] inside the default run: PySwizzle.prove (PySwizzle.py:333-370)
+    of a 10,000-index challenge over the encode's own device-resident file and
+    tags -- the same call as `--config c5`, `proofs` timed back to back after
+    20 warm-ups.  Checked against the oracle without copying the file back:
+    the oracle's KeyedPRF(key, #tags) gives the challenged indices
+    (PySwizzle.py:344-345), only those blocks and tags are copied into an
+    otherwise untouched (lazily zero) host image, and oracle/swizzle_oracle.c
+    and the native CPU prove (baseline/hb_cpu_swizzle.cpp) prove on it."""
+    from heartbeat_amd import _native
+    pb = _native.be(p)
+    ck = hashlib.sha256(b"hb-bench-challenge").digest()
+    mu = ctypes.create_string_buffer(w * S)
+    sg = ctypes.create_string_buffer(w)
+
+    def one():
+        ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, ck, len(ck), chunks, pb, len(pb), tptr, nblocks, dptr, length,
+                             3, mu, sg))
+
+    for _ in range(min(20, proofs)):
+        one()
+    t = time.perf_counter()
+    for _ in range(proofs):
+        one()
+    ms = (time.perf_counter() - t) / proofs * 1e3
+    launches = ctx.last_kernel_ms()[1]
+    gib = length / GIB
+    row = {"workload": "configs[4]: Swizzle prove() on this run's %g GiB device-resident file and tags, "
+                       "10 000-index challenge, 256-bit prime, 16 sectors/block, 1 MI355X%s"
+                       % (gib, "" if gib == 64 else " [not configs[4]'s 64 GiB]"),
+           "ms_per_proof": round(ms, 4), "proofs": proofs, "chunks": chunks,
+           "launches_per_proof": launches,
+           "path": "fused PRF + weighted-sum launch (DESIGN.md 5.3)" if launches == 1 else
+                   "PRF launch + hb_wsum_kernel"}
+    if args.no_cpu_baseline:
+        return row
+    import numpy as np
+    from oracle import oracle as O
+    idx = sorted({O.prf_eval(ck, nblocks, i) for i in range(chunks)})
+    host = np.zeros(length, dtype=np.uint8)          # untouched pages stay unallocated
+    tags = np.zeros(nblocks * w, dtype=np.uint8)
+    for ix in idx:
+        a = ix * C
+        if a < length:
+            ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data + a, dptr.value + a, min(C, length - a), 2))
+        ctx.check(L.hb_memcpy(ctx.h, tags.ctypes.data + ix * w, tptr.value + ix * w, w, 2))
+    ref_mu = ctypes.create_string_buffer(w * S)
+    ref_sg = ctypes.create_string_buffer(w)
+    rc = O.lib().hbo_prove(pb, len(pb), S, ck, len(ck), chunks, pb, len(pb), nblocks,
+                           ctypes.cast(tags.ctypes.data, ctypes.c_char_p), w, host.ctypes.data, length, ref_mu, ref_sg)
+    if rc:
+        raise RuntimeError("oracle prove error %d" % rc)
+    row["proof_equal_oracle"] = ref_mu.raw == mu.raw and ref_sg.raw == sg.raw
+    row["oracle_check"] = ("%d distinct challenged blocks and tags copied back; oracle/swizzle_oracle.c proves on "
+                           "them (indices from its own KeyedPRF)" % len(idx))
+    from baseline import cpu as NC
+    info = host_cpu_info()
+    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS") or info.get("affinity") or
+                                      os.cpu_count() or 1)
+    want_mu = [int.from_bytes(mu.raw[j * w:(j + 1) * w], "big") for j in range(S)]
+    for th in sorted({1, threads}):
+        NC.prove_raw(p, S, ck, chunks, p, nblocks, tags.ctypes.data, host.ctypes.data, length, th)   # warm-up
+        t = time.perf_counter()
+        k = 0
+        while k < 3 or time.perf_counter() - t < 1.0:
+            nmu, nsg = NC.prove_raw(p, S, ck, chunks, p, nblocks, tags.ctypes.data, host.ctypes.data, length, th)
+            k += 1
+        row["cpu_native_%d_threads_ms" % th] = round((time.perf_counter() - t) / k * 1e3, 4)
+        row["cpu_native_equal_gpu"] = nmu == want_mu and nsg == int.from_bytes(sg.raw, "big")
+    row["cpu_native"] = ("baseline/hb_cpu_swizzle.cpp prove (the cxx Swizzle counterpart) on the same host image, "
+                         "1 and %d std::threads" % threads)
+    return row
 
 
 def _native_flag(name):

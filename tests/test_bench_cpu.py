@@ -37,13 +37,17 @@ def test_default_encode_line_with_every_leg(fake, monkeypatch, capsys, tmp_path)
     monkeypatch.setenv("TMPDIR", str(tmp_path))
     monkeypatch.setenv("OMP_NUM_THREADS", "4")
     d = _run_bench(monkeypatch, capsys, "--gib", "0.001", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3",
-                   "--py-seconds", "0.2", "--sustain-seconds", "0.05", "--parity-blocks", "100")
+                   "--py-seconds", "0.2", "--sustain-seconds", "0.05", "--parity-blocks", "100",
+                   "--prove-proofs", "2")
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["unit"] == "GiB/s"
     assert "[--gib 0.001" in d["config"]["workload"]
     assert d["parity_sample"]["ok"] is True
     assert d["cpu_baseline"]["tags_equal_gpu"] is True
     assert d["cpu_baseline"]["oracle_row"]["tags_equal_gpu"] is True
     assert d["sustained"]["steps"] >= 1
+    pr = d["prove"]
+    assert pr["proof_equal_oracle"] is True and pr["cpu_native_equal_gpu"] is True and pr["proofs"] == 2
+    assert pr["workload"].startswith("configs[4]")
     assert d["build"]["build_id"] == "0" * 64
     hp = d["host_path"]
     assert hp["raw_tags_equal"] is True and hp["api_tags_equal"] is True
