@@ -474,7 +474,8 @@ def bench_encode(args, cfg, R):
     # reuse the device buffer
     if R.rank == 0 and R.world == 1 and args.config == "c3" and not cxx and not args.no_prove and len(pieces) == 1:
         t = time.perf_counter()
-        line["prove"] = prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, proofs=args.prove_proofs)
+        line["prove"] = prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, fk, ak,
+                                  proofs=args.prove_proofs)
         line["prove"]["seconds_spent"] = round(time.perf_counter() - t, 1)
     # the host-memory rows come right after the device-resident ones: after
     # the CPU rows (16 threads streaming 64 GiB through host buffers) the same
@@ -891,7 +892,27 @@ def host_path(ctx, L, dptr, length, S, pb, fk, ak, C):
     return out
 
 
-def prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, proofs=200, chunks=10000):
+def verify_timing(ctx, L, pb, S, fk, ak, nblocks, ck, chunks, mu, sg, reps):
+    """PySwizzle.verify (PySwizzle.py:372-395) of that proof, timed: the
+    right-hand side sum_i v_i F(idx_i) + sum_j alpha_j mu_j on the GPU
+    (hb_verify_rhs), compared with sigma."""
+    w = len(sg.raw)
+    rhs = ctypes.create_string_buffer(w)
+
+    def one():
+        ctx.check(L.hb_verify_rhs(ctx.h, pb, len(pb), S, fk, ak, len(fk), nblocks, ck, len(ck), chunks, pb, len(pb),
+                                  mu.raw, rhs))
+
+    for _ in range(min(10, reps)):
+        one()
+    t = time.perf_counter()
+    for _ in range(reps):
+        one()
+    return {"ms_per_verify": round((time.perf_counter() - t) / reps * 1e3, 4), "verifies": reps,
+            "verified": rhs.raw == sg.raw}
+
+
+def prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, fk, ak, proofs=200, chunks=10000):
     """configs[4] inside the default run: PySwizzle.prove (PySwizzle.py:333-370)
     of a 10,000-index challenge over the encode's own device-resident file and
     tags -- the same call as `--config c5`, `proofs` timed back to back after
@@ -925,6 +946,7 @@ def prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, proofs=200,
            "launches_per_proof": launches,
            "path": "fused PRF + weighted-sum launch (DESIGN.md 5.3)" if launches == 1 else
                    "PRF launch + hb_wsum_kernel"}
+    row["verify"] = verify_timing(ctx, L, pb, S, fk, ak, nblocks, ck, chunks, mu, sg, max(2, proofs // 4))
     if args.no_cpu_baseline:
         return row
     import numpy as np
@@ -1027,6 +1049,8 @@ def bench_prove(args, cfg, R):
         "gathered_bytes_per_proof": chunks * (C + w),
         "build": _native.build_info(),
     }
+    if not cxx:
+        line["verify"] = verify_timing(ctx, L, pb, S, fk, ak, nblocks, ck, chunks, mu, sg, max(2, steps // 4))
     if R.rank == 0 and not args.no_cpu_baseline and not cxx:
         import numpy as np
         from oracle import oracle as O

@@ -1415,8 +1415,12 @@ __device__ __forceinline__ void hb_fused_sum(const ProveArgs<NL> &A, const HbFz 
         __hip_atomic_store(A.flags, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(A.fctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         A.fout[(u64)nc * NL] = st;
-        A.fout[(u64)nc * NL + 1] = A.ftoken;
     }
+    // the token last, after a system-scope release: the host may poll it in
+    // the pinned buffer and read the sums as soon as it changes (finish_sums)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (hb_lane_id() == 0)
+        __hip_atomic_store(A.fout + (u64)nc * NL + 1, A.ftoken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <int NL, int NR>

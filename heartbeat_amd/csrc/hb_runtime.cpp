@@ -18,6 +18,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -122,6 +123,7 @@ struct hb_ctx {
     std::string err;
     double last_ms = 0.0;
     u32 last_launches = 0;
+    bool sums_polled = false;   // the last sum was a fused prove's: finish_sums polls its token
     hipStream_t own_stream = nullptr;   // `stream` unless hb_ctx_set_stream gave another
     // an HB_ASYNC encode still running: its counters, and the status and tries
     // of the last one completed (hb_ctx_wait)
@@ -187,6 +189,7 @@ const SwitchName kSwitches[] = {
     {"HB_SUMS_ON_DEVICE", HB_SW_SUMS_ON_DEVICE},
     {"HB_NO_PROVE_PLACE", HB_SW_NO_PROVE_PLACE},
     {"HB_NO_PROVE_FUSE", HB_SW_NO_PROVE_FUSE},
+    {"HB_SYNC_WAIT", HB_SW_SYNC_WAIT},
 };
 
 int nl_for_bits(int bits) {
@@ -1138,7 +1141,9 @@ int ensure_hres(hb_ctx *c, size_t words) {
     if (c->hres) (void)hipHostFree(c->hres);
     c->hres = nullptr;
     c->hres_n = 0;
-    HB_CHECK(hipHostMalloc((void **)&c->hres, words * 4, 0), "hipHostMalloc");
+    // coherent: a fused prove's host polls the completion token while the
+    // kernel still runs (finish_sums)
+    HB_CHECK(hipHostMalloc((void **)&c->hres, words * 4, hipHostMallocCoherent), "hipHostMalloc");
     c->hres_n = words;
     return 0;
 }
@@ -1184,6 +1189,7 @@ int launch_wsum(hb_ctx *c, WsumArgs<NL> &A, int align) {
     // the sum.  $HB_SUMS_ON_DEVICE (test switch, A/B): device buffer + copy.
     const size_t words = (size_t)A.ncols * NL + 2;
     c->sums_in_hres = !sw_env(c, "HB_SUMS_ON_DEVICE");
+    c->sums_polled = false;
     if (c->sums_in_hres) {
         if (int rc = ensure_hres(c, words)) return rc;
         A.out = c->hres;
@@ -1205,9 +1211,30 @@ int finish_sums(hb_ctx *c, u32 ncols, u32 tw, uint8_t *out, bool cxx_index_check
         if (int rc = ensure_hres(c, words)) return rc;
         HB_CHECK(hipMemcpyAsync(c->hres, c->sums.p, words * 4, hipMemcpyDeviceToHost, c->stream), "hipMemcpy");
     }
-    // (a polled wait -- hipEventQuery in a loop -- measured slower than this
-    // blocking one: 0.2118 vs 0.2041 ms per configs[4] proof, profiles/r05/j)
-    HB_CHECK(hipStreamSynchronize(c->stream), "prove");
+    if (c->sums_polled && !sw_env(c, "HB_SYNC_WAIT")) {
+        // A fused prove writes its sums, status word and (after a system-scope
+        // release) the completion token into the coherent pinned buffer from
+        // the kernel's last wave: watch the token word itself instead of
+        // waiting for the stream -- no completion signal and thread wake-up
+        // on the prove's critical path.  Bounded by the stream: once it has
+        // drained (or failed), a missing token is the mismatch below.
+        // ($HB_SYNC_WAIT, test switch: hipStreamSynchronize as before.)
+        const volatile u32 *tok = c->hres + (size_t)ncols * NL + 1;
+        for (u32 spins = 1; *tok != c->wsum_token; ++spins) {
+            if ((spins & 255u) == 0) {
+                const hipError_t q = hipStreamQuery(c->stream);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) HB_CHECK(q, "prove");
+            }
+            __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    } else {
+        // (a polled wait -- hipEventQuery in a loop -- measured slower than
+        // this blocking one: 0.2118 vs 0.2041 ms per configs[4] proof,
+        // profiles/r05/j)
+        HB_CHECK(hipStreamSynchronize(c->stream), "prove");
+    }
     if (c->hres[(size_t)ncols * NL + 1] != c->wsum_token) {
         // some column's finisher (or a batch) did not run: out[] is not this
         // operation's result (hb_wsum_kernel, I1).  Loud, and the counters are
@@ -1402,6 +1429,7 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         const size_t words = (size_t)ncols * NL + 2;
         if (int rc = ensure_hres(c, words)) return rc;
         c->sums_in_hres = true;
+        c->sums_polled = true;
         PA.fuse = 1u;
         PA.ncols = ncols;
         PA.fcmax = (u32)fcmax;

@@ -117,6 +117,7 @@ const char *hb_build_flags_string(void);
 #define HB_SW_SUMS_ON_DEVICE 2048u   /* HB_SUMS_ON_DEVICE: weighted sums land in device memory + a D2H copy */
 #define HB_SW_NO_PROVE_PLACE 4096u   /* HB_NO_PROVE_PLACE: prove PRF waves take jobs from the queue, not by SIMD */
 #define HB_SW_NO_PROVE_FUSE 8192u    /* HB_NO_PROVE_FUSE: device proves sum in a second launch (hb_wsum_kernel) */
+#define HB_SW_SYNC_WAIT 16384u       /* HB_SYNC_WAIT: a fused prove waits for its stream instead of polling its token */
 uint32_t hb_test_switches(void);
 
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens

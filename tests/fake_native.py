@@ -123,6 +123,27 @@ class FakeLib(object):
         return O.lib().hbo_prove(bytes(pb[:plen]), plen, S, bytes(key[:klen]), klen, chunks, bytes(vb[:vlen]), vlen,
                                  ntags, ctypes.cast(_v(tags), ctypes.c_char_p), w, _v(data) or 0, int(length), mu, sg)
 
+    def hb_verify_rhs(self, h, pb, plen, S, fk, ak, klen, nchunks, key, kl2, chunks, vb, vlen, mu, rhs):
+        """sum_i v_i F(idx_i) + sum_j alpha_j mu_j mod p (PySwizzle.py:380-395)
+        from the oracle's KeyedPRF, memoised per argument set."""
+        from oracle import oracle as O
+        p = int.from_bytes(bytes(pb[:plen]), "big")
+        w = (p.bit_length() + 7) // 8
+        arg = (bytes(pb[:plen]), S, bytes(fk[:klen]), bytes(ak[:klen]), nchunks, bytes(key[:kl2]), chunks,
+               bytes(vb[:vlen]), bytes(mu[:S * w]))
+        memo = self.__dict__.setdefault("_rhs", {})
+        if arg not in memo:
+            vmax = int.from_bytes(bytes(vb[:vlen]), "big")
+            r = 0
+            for i in range(chunks):
+                ix = O.prf_eval(arg[5], nchunks, i)
+                r += O.prf_eval(arg[5], vmax, i) * O.prf_eval(arg[2], p, ix)
+            for j in range(S):
+                r += O.prf_eval(arg[3], p, j) * int.from_bytes(arg[8][j * w:(j + 1) * w], "big")
+            memo[arg] = r % p
+        ctypes.memmove(rhs, memo[arg].to_bytes(w, "big"), w)
+        return 0
+
     def hb_prove(self, h, pb, plen, S, key, klen, chunks, vb, vlen, tags, ntags, data, length, flags, mu, sg):
         return self.hb_prove_range(h, pb, plen, S, key, klen, chunks, 0, chunks, vb, vlen, tags, ntags, data,
                                    length, flags, mu, sg)

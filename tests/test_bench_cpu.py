@@ -48,6 +48,7 @@ def test_default_encode_line_with_every_leg(fake, monkeypatch, capsys, tmp_path)
     pr = d["prove"]
     assert pr["proof_equal_oracle"] is True and pr["cpu_native_equal_gpu"] is True and pr["proofs"] == 2
     assert pr["workload"].startswith("configs[4]")
+    assert pr["verify"]["verified"] is True
     assert d["build"]["build_id"] == "0" * 64
     hp = d["host_path"]
     assert hp["raw_tags_equal"] is True and hp["api_tags_equal"] is True
@@ -75,6 +76,7 @@ def test_prove_line(fake, monkeypatch, capsys):
     assert d["unit"] == "ms" and d["higher_is_better"] is False
     assert d["proof_equal_oracle"] is True
     assert d["cpu_baseline"]["proof_equal_gpu"] is True
+    assert d["verify"]["verified"] is True
 
 
 def test_two_rank_encode_line(tmp_path):
