@@ -170,6 +170,29 @@ struct ProveArgs {
     u32 *fout;                    // [ncols][NL] results, the status word, the token word
 };
 
+// The fused verify (hb_verify_fused_kernel): rhs = sum_i v_i F(idx_i) + sum_j
+// alpha_j mu_j mod p (PySwizzle.py:380-395) in one launch, all four PRF
+// keys with the same AES round count (NR, a template parameter).
+template <int NL>
+struct VerifyArgs {
+    PrfParams<2> pi;              // idx = KeyedPRF(chal_key, #state chunks)
+    PrfParams<NL> pv;             // v = KeyedPRF(chal_key, v_max)
+    PrfParams<NL> pf;             // F = KeyedPRF(f_key, p) of idx
+    PrfParams<NL> pa;             // alpha = KeyedPRF(alpha_key, p)
+    ModP<NL> mod;
+    u32 r2[NL];                   // R^2 mod p
+    u64 i0, n, ntags;             // challenge indices [i0, i0 + n)
+    u32 S, fcmax, ftoken, pad_;
+    const u32 *mu;                // S x NL limbs, pinned host memory
+    const u32 *t0;
+    unsigned long long *queue;    // 4 engine slots: idx, v, F, alpha (zero between launches)
+    unsigned int *flags;
+    u64 qchunk;
+    unsigned long long *facc;     // [NL] limb sums over workgroups, zero between launches
+    unsigned int *fctl;           // finished-workgroup counter
+    u32 *fout;                    // [NL] rhs, the status word, the token word
+};
+
 // The fused prove's LDS arena (next to the 128 KiB T-table image): byte
 // offsets of [0] the per-job index / v ready flags (2 cmax words) and 4
 // counters, [1] the v slots (cmax x NL words), [2] the workgroup's limb sums

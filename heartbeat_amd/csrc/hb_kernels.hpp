@@ -1292,9 +1292,9 @@ struct FusedIdxHandler {
     __device__ __forceinline__ void fail(u64 job) const { gather(job, A.ntags); }   // zeros; status bit 2
 };
 
-template <int NL>
+template <int NL, class ARGS = ProveArgs<NL>>
 struct FusedVHandler {
-    const ProveArgs<NL> &A;
+    const ARGS &A;
     const HbFz &z;
     u64 j0;
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.i0 + job; }
@@ -1313,15 +1313,100 @@ struct FusedVHandler {
     }
 };
 
+// The common end of a fused launch's summer waves (12 .. 15): each summer
+// lane that had terms (have) reduces its sum once and adds the residue into
+// the workgroup's per-column u64 limb sums in LDS; when all four summer waves
+// and the workgroup's nprod producer waves have signalled, wave 12 adds the
+// limb sums into the global ones and bumps the workgroup counter; the last
+// workgroup carries and reduces the nc sums (< 2^16 p), writes them, the
+// status word (bit 1: a PRF job abandoned in any of the nslots engine slots;
+// flags bits 0 and 2) and -- after a system-scope release -- the completion
+// token into `out`, and re-zeroes facc, the counter, the slots and the flags.
+template <int NL>
+__device__ __forceinline__ void hb_fused_close(const ModP<NL> &mod, const HbFz &z, bool have, u32 acc[2 * NL + 1],
+                                               u32 col, bool timeout, u32 nc, u32 nprod,
+                                               unsigned long long *facc, unsigned int *fctl, u32 *out, u32 token,
+                                               unsigned long long *qslots, u32 nslots, unsigned int *flags) {
+    if (have) {
+        u32 v[NL + 1], res[NL];
+        hb_redc<NL>(acc, mod, v);
+        hb_reduce_small<NL>(v, mod, res);
+        for (int t = 0; t < NL; ++t)
+            __hip_atomic_fetch_add(z.acc + col * NL + t, (unsigned long long)res[t], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (__ballot(timeout)) {
+        if (hb_lane_id() == 0) __hip_atomic_store(z.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (hb_lane_id() == 0) __hip_atomic_fetch_add(z.ctr + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (threadIdx.x >> 6 != 12) return;
+    // wave 12: every summer and producer wave of this workgroup has signalled
+    u32 spins = 0;
+    while (__hip_atomic_load(z.ctr + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u ||
+           __hip_atomic_load(z.ctr + 0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < nprod) {
+        if (++spins > HB_FUSE_SPINS) {
+            timeout = true;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    for (u32 i = hb_lane_id(); i < nc * NL; i += 64) {
+        const unsigned long long x = __hip_atomic_load(z.acc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (x) __hip_atomic_fetch_add(facc + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const bool to = __ballot(timeout) != 0 || __hip_atomic_load(z.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (to && hb_lane_id() == 0) atomicOr(flags, 4u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    u32 lastw = 0;
+    if (hb_lane_id() == 0)
+        lastw = __hip_atomic_fetch_add(fctl, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x;
+    if (!__builtin_amdgcn_readfirstlane(lastw)) return;
+    // the last workgroup: carry, reduce and write the nc sums, re-zero
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (u32 c = hb_lane_id(); c < nc; c += 64) {
+        u32 v[NL + 1], o[NL];
+        u64 carry = 0;
+        for (int t = 0; t < NL; ++t) {
+            unsigned long long *a = facc + c * NL + t;
+            carry += __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[t] = (u32)carry;
+            carry >>= 32;
+        }
+        v[NL] = (u32)carry;      // < 2^16 p in all: <= 256 residues < p per workgroup
+        hb_reduce_small<NL>(v, mod, o);
+        for (int t = 0; t < NL; ++t) out[(u64)c * NL + t] = o[t];
+    }
+    if (hb_lane_id() == 0) {
+        u32 st = 0;
+        for (u32 q = 0; q < nslots; ++q) {
+            unsigned long long *qs = qslots + (u64)q * HB_QSLOT;
+            st |= __hip_atomic_load(qs + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 2u : 0u;
+            for (int k2 = 0; k2 < HB_QSLOT; ++k2) __hip_atomic_store(qs + k2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const u32 fl = __hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st |= (fl & 1u) | ((fl & 4u) ? 4u : 0u);
+        __hip_atomic_store(flags, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        out[(u64)nc * NL] = st;
+    }
+    // the token last, after a system-scope release: the host may poll it in
+    // the pinned buffer and read the sums as soon as it changes (finish_sums)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (hb_lane_id() == 0)
+        __hip_atomic_store(out + (u64)nc * NL + 1, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Summer wave (12 .. 15) of the fused prove.
 template <int NL>
 __device__ __forceinline__ void hb_fused_sum(const ProveArgs<NL> &A, const HbFz &z, u64 j0, u64 j1) {
     const u32 l = threadIdx.x - 12u * 64u, nc = A.ncols, R = 256u / nc;
     const u32 col = l % nc, r = l / nc, cnt = (u32)(j1 - j0);
     bool timeout = false;
+    u32 acc[2 * NL + 1];
+    for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
     if (r < R) {
-        u32 acc[2 * NL + 1];
-        for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
         u64 pending = 0;
         for (u32 k = r; k < cnt; k += R) pending |= 1ull << k;
         u32 spins = 0;
@@ -1353,74 +1438,9 @@ __device__ __forceinline__ void hb_fused_sum(const ProveArgs<NL> &A, const HbFz 
                 __builtin_amdgcn_s_sleep(2);
             }
         }
-        u32 v[NL + 1], res[NL];
-        hb_redc<NL>(acc, A.mod, v);
-        hb_reduce_small<NL>(v, A.mod, res);
-        for (int t = 0; t < NL; ++t)
-            __hip_atomic_fetch_add(z.acc + col * NL + t, (unsigned long long)res[t], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (__ballot(timeout)) {
-        if (hb_lane_id() == 0) __hip_atomic_store(z.ctr + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (hb_lane_id() == 0) __hip_atomic_fetch_add(z.ctr + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (threadIdx.x >> 6 != 12) return;
-    // wave 12: every summer and producer wave of this workgroup has signalled
-    u32 spins = 0;
-    while (__hip_atomic_load(z.ctr + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u ||
-           __hip_atomic_load(z.ctr + 0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 6u) {
-        if (++spins > HB_FUSE_SPINS) {
-            timeout = true;
-            break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-    for (u32 i = hb_lane_id(); i < nc * NL; i += 64) {
-        const unsigned long long x = __hip_atomic_load(z.acc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (x) __hip_atomic_fetch_add(A.facc + i, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const bool to = __ballot(timeout) != 0 || __hip_atomic_load(z.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (to && hb_lane_id() == 0) atomicOr(A.flags, 4u);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    u32 lastw = 0;
-    if (hb_lane_id() == 0)
-        lastw = __hip_atomic_fetch_add(A.fctl, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x;
-    if (!__builtin_amdgcn_readfirstlane(lastw)) return;
-    // the last workgroup: carry, reduce and write the ncols sums, re-zero
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    for (u32 c = hb_lane_id(); c < nc; c += 64) {
-        u32 v[NL + 1], o[NL];
-        u64 carry = 0;
-        for (int t = 0; t < NL; ++t) {
-            unsigned long long *a = A.facc + c * NL + t;
-            carry += __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v[t] = (u32)carry;
-            carry >>= 32;
-        }
-        v[NL] = (u32)carry;      // < 2^16 p in all: 255 residues < p per workgroup
-        hb_reduce_small<NL>(v, A.mod, o);
-        for (int t = 0; t < NL; ++t) A.fout[(u64)c * NL + t] = o[t];
-    }
-    if (hb_lane_id() == 0) {
-        u32 st = 0;
-        for (u32 q = 0; q < 2; ++q) {
-            unsigned long long *qs = A.queue + (u64)q * HB_QSLOT;
-            st |= __hip_atomic_load(qs + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 2u : 0u;
-            for (int k2 = 0; k2 < HB_QSLOT; ++k2) __hip_atomic_store(qs + k2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const u32 fl = __hip_atomic_load(A.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        st |= (fl & 1u) | ((fl & 4u) ? 4u : 0u);
-        __hip_atomic_store(A.flags, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(A.fctl, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        A.fout[(u64)nc * NL] = st;
-    }
-    // the token last, after a system-scope release: the host may poll it in
-    // the pinned buffer and read the sums as soon as it changes (finish_sums)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    if (hb_lane_id() == 0)
-        __hip_atomic_store(A.fout + (u64)nc * NL + 1, A.ftoken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    hb_fused_close<NL>(A.mod, z, r < R, acc, col, timeout, nc, 6u, A.facc, A.fctl, A.fout, A.ftoken, A.queue, 2u,
+                       A.flags);
 }
 
 template <int NL, int NR>
@@ -1445,6 +1465,150 @@ __device__ __forceinline__ void hb_prove_fused(const ProveArgs<NL> &A, const Lan
         if (hb_lane_id() == 0) __hip_atomic_fetch_add(z.ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else if (w >= 12) {
         hb_fused_sum<NL>(A, z, j0, j1);
+    }
+}
+
+// ------------------------------------------------------------------ fused verify
+// PySwizzle.verify's right-hand side (PySwizzle.py:380-395) in one launch,
+// on the fused prove's scheme (hb_prove_fused): workgroup g owns challenge
+// jobs [n g / G, n (g + 1) / G) (<= 48);
+//   waves 0-2  v = KeyedPRF(chal_key, v_max)(i), v R mod p into LDS (+ flag)
+//   waves 3-5  idx = KeyedPRF(chal_key, #chunks)(i) for their 16 jobs, then
+//              F = KeyedPRF(f_key, p)(idx) (a quad engine over the same jobs
+//              whose inputs are those indices) into LDS (+ flag): serial in
+//              the wave, the index chains being ~1/4 of an F chain
+//   wave 6     alpha_j = KeyedPRF(alpha_key, p)(j), j in [16 g, 16 g + 16) of
+//              [0, S), and the terms alpha_j mu_j straight into the
+//              workgroup's limb sums
+//   waves 12-15 summers: lane k adds v_k F_k as soon as both are there.
+// 7 producer waves signal; the close is hb_fused_close's (one column).
+// Long chains: 3 v + 3 F waves per CU on its 4 SIMDs (waves 3..5 sit on
+// SIMDs 3, 0, 1), so two SIMDs host two.
+template <int NL>
+__device__ __forceinline__ HbFz hb_fz_verify(unsigned char *base, const VerifyArgs<NL> &A) {
+    u32 off[5];
+    hb_fz_layout(A.fcmax, NL, 1, 4ull * NL, 8, off);   // "blocks": F slots, "tags": index slots
+    HbFz z;
+    z.iflag = (u32 *)base;       // F ready
+    z.vflag = z.iflag + A.fcmax;
+    z.ctr = z.vflag + A.fcmax;
+    z.v = (u32 *)(base + off[1]);
+    z.acc = (unsigned long long *)(base + off[2]);
+    z.blk = base + off[3];
+    z.tag = base + off[4];
+    return z;
+}
+
+template <int NL>
+struct VerifyIdxHandler {
+    const VerifyArgs<NL> &A;
+    const HbFz &z;
+    u64 j0;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return A.i0 + job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void accept(u64 job, const u32 v[2]) const {
+        reinterpret_cast<u64 *>(z.tag)[job - j0] = (u64)v[0] | ((u64)v[1] << 32);
+    }
+    __device__ __forceinline__ void fail(u64 job) const { reinterpret_cast<u64 *>(z.tag)[job - j0] = 0; }
+};
+
+template <int NL>
+struct VerifyFHandler {   // F(idx) (PySwizzle.py:389): the input is the job's index
+    const VerifyArgs<NL> &A;
+    const HbFz &z;
+    u64 j0;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return reinterpret_cast<const u64 *>(z.tag)[job - j0]; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void accept(u64 job, const u32 f[NL]) const {
+        u32 *o = reinterpret_cast<u32 *>(z.blk) + (job - j0) * NL;
+        for (int t = 0; t < NL; ++t) o[t] = f[t];
+        hb_fz_raise(z.iflag + (job - j0));
+    }
+    __device__ __forceinline__ void fail(u64 job) const {
+        u32 *o = reinterpret_cast<u32 *>(z.blk) + (job - j0) * NL;
+        for (int t = 0; t < NL; ++t) o[t] = 0;
+        hb_fz_raise(z.iflag + (job - j0));
+    }
+};
+
+template <int NL>
+struct VerifyAlphaHandler {   // alpha_j mu_j (PySwizzle.py:392) into the limb sums
+    const VerifyArgs<NL> &A;
+    const HbFz &z;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void accept(u64 job, const u32 a[NL]) const {
+        u32 y[NL], m[NL], acc[2 * NL + 1], v[NL + 1], res[NL];
+        hb_to_mont<NL>(a, A.r2, A.mod, y);
+        for (int t = 0; t < NL; ++t) m[t] = A.mu[job * NL + t];
+        for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
+        hb_mac<NL>(acc, y, m);
+        hb_redc<NL>(acc, A.mod, v);
+        hb_reduce_small<NL>(v, A.mod, res);
+        for (int t = 0; t < NL; ++t)
+            __hip_atomic_fetch_add(z.acc + t, (unsigned long long)res[t], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __device__ __forceinline__ void fail(u64) const {}   // status bit 1 (abandoned job)
+};
+
+template <int NL, int NR>
+__global__ __launch_bounds__(HB_ENGINE_WG) void hb_verify_fused_kernel(VerifyArgs<NL> A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    __shared__ __attribute__((aligned(16))) unsigned char fz[HB_FZ_BYTES];
+    const HbFz z = hb_fz_verify<NL>(fz, A);
+    for (u32 i = threadIdx.x; i < 2 * A.fcmax + 4; i += blockDim.x) z.iflag[i] = 0;
+    for (u32 i = threadIdx.x; i < NL; i += blockDim.x) z.acc[i] = 0;
+    hb_fill_lds(lds, A.t0);
+    const LaneTab L = hb_lane_tab(lds);
+    const u64 G = gridDim.x, g = blockIdx.x;
+    const u64 j0 = A.n * g / G, j1 = A.n * (g + 1) / G;
+    const u32 w = threadIdx.x >> 6;
+    if (w < 7) {
+        if (w < 3) {
+            const u64 first = j0 + 16ull * w;
+            if (first < j1) {
+                FusedVHandler<NL, VerifyArgs<NL>> h{A, z, j0};
+                hb_engine_quad<NL, NR, FusedVHandler<NL, VerifyArgs<NL>>>(h, L, A.pv, A.n, A.queue + HB_QSLOT,
+                                                                          A.qchunk, first, j1);
+            }
+        } else if (w < 6) {
+            const u64 first = j0 + 16ull * (w - 3);
+            if (first < j1) {
+                VerifyIdxHandler<NL> hi{A, z, j0};
+                hb_engine_quad<2, NR, VerifyIdxHandler<NL>>(hi, L, A.pi, A.n, A.queue, A.qchunk, first, j1);
+                VerifyFHandler<NL> hf{A, z, j0};
+                hb_engine_quad<NL, NR, VerifyFHandler<NL>>(hf, L, A.pf, A.n, A.queue + 2 * HB_QSLOT, A.qchunk, first,
+                                                           j1);
+            }
+        } else {
+            const u64 first = 16ull * g;
+            if (first < A.S) {
+                VerifyAlphaHandler<NL> ha{A, z};
+                hb_engine_quad<NL, NR, VerifyAlphaHandler<NL>>(ha, L, A.pa, A.S, A.queue + 3 * HB_QSLOT, A.qchunk,
+                                                               first, A.S);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (hb_lane_id() == 0) __hip_atomic_fetch_add(z.ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else if (w >= 12) {
+        const u32 k = threadIdx.x - 12u * 64u, cnt = (u32)(j1 - j0);
+        bool timeout = false;
+        u32 acc[2 * NL + 1];
+        for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
+        if (k < cnt) {
+            u32 spins = 0;
+            while (!hb_fz_get(z.vflag + k) || !hb_fz_get(z.iflag + k)) {
+                if (++spins > HB_FUSE_SPINS) {
+                    timeout = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!timeout) hb_mac<NL>(acc, z.v + (u64)k * NL, reinterpret_cast<const u32 *>(z.blk) + (u64)k * NL);
+        }
+        hb_fused_close<NL>(A.mod, z, k < cnt, acc, 0u, timeout, 1u, 7u, A.facc, A.fctl, A.fout, A.ftoken, A.queue,
+                           4u, A.flags);
     }
 }
 
@@ -1804,6 +1968,16 @@ hipError_t hb_launch_prove_prf(const ProveArgs<NL> &A, int nr, int mode_i, int m
     return hipGetLastError();
 }
 
+// fused verify (NL <= 16; every key with nr AES rounds)
+template <int NL>
+hipError_t hb_launch_verify_fused(const VerifyArgs<NL> &A, int nr, int grid, hipStream_t s) {
+    dim3 g(grid), b(HB_ENGINE_WG);
+    if (nr == 14) HB_LAUNCH((hb_verify_fused_kernel<NL, 14>), g, b, s, A);
+    else if (nr == 12) HB_LAUNCH((hb_verify_fused_kernel<NL, 12>), g, b, s, A);
+    else HB_LAUNCH((hb_verify_fused_kernel<NL, 10>), g, b, s, A);
+    return hipGetLastError();
+}
+
 // Explicit instantiations per limb count; the encode and the PRF / prove
 // halves can go to separate translation units (parallel builds of the
 // slow-to-compile wide-limb kernels).
@@ -1822,4 +1996,6 @@ hipError_t hb_launch_prove_prf(const ProveArgs<NL> &A, int nr, int mode_i, int m
     template hipError_t hb_launch_mont<NL>(const MontArgs<NL> &, hipStream_t);                   \
     template hipError_t hb_launch_wsum<NL>(const WsumArgs<NL> &, int, int, hipStream_t);         \
     template hipError_t hb_launch_prove_prf<NL>(const ProveArgs<NL> &, int, int, int, int, hipStream_t);
+#define HB_INST_VERIFY_FUSED(NL) \
+    template hipError_t hb_launch_verify_fused<NL>(const VerifyArgs<NL> &, int, int, hipStream_t);
 #define HB_INST(NL) HB_INST_ENC(NL) HB_INST_PRF(NL)

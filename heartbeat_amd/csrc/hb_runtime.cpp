@@ -36,6 +36,7 @@ template <int NL> hipError_t hb_launch_prf(const PrfArgs<NL> &, int, int, int, h
 template <int NL> hipError_t hb_launch_mont(const MontArgs<NL> &, hipStream_t);
 template <int NL> hipError_t hb_launch_wsum(const WsumArgs<NL> &, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_prove_prf(const ProveArgs<NL> &, int, int, int, int, hipStream_t);
+template <int NL> hipError_t hb_launch_verify_fused(const VerifyArgs<NL> &, int, int, hipStream_t);
 hipError_t hb_launch_fill(unsigned char *, u64, u64, hipStream_t);
 hipError_t hb_launch_read(const void *, u64, u32 *, int, hipStream_t);
 hipError_t hb_launch_merkle_offsets(const MerkleArgs &, int, hipStream_t);
@@ -109,6 +110,7 @@ struct hb_ctx {
     bool h2d_pending = false;
     bool alpha_pending = false;   // the alpha D2H into hscratch not yet waited for
     bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
+    bool verify_dirty = false;  // a fused verify did not complete: its slots and sums to clear
     bool ctl_dirty = false;     // a weighted sum did not complete: clear its counters
     u32 wsum_token = 0;         // completion token of the last hb_wsum_kernel launch
     // HB_ENABLE_TEST_SWITCHES=1 when the context was created: the A/B and test
@@ -190,6 +192,7 @@ const SwitchName kSwitches[] = {
     {"HB_NO_PROVE_PLACE", HB_SW_NO_PROVE_PLACE},
     {"HB_NO_PROVE_FUSE", HB_SW_NO_PROVE_FUSE},
     {"HB_SYNC_WAIT", HB_SW_SYNC_WAIT},
+    {"HB_NO_VERIFY_FUSE", HB_SW_NO_VERIFY_FUSE},
 };
 
 int nl_for_bits(int bits) {
@@ -1244,6 +1247,10 @@ int finish_sums(hb_ctx *c, u32 ncols, u32 tw, uint8_t *out, bool cxx_index_check
     }
     const u32 st = c->hres[(size_t)ncols * NL];
     if (st & 2u) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate");
+    if (st & 4u) {   // a fused launch's bounded wait ran out (hb_fused_close): its counters are suspect
+        c->ctl_dirty = true;
+        return fail(c, HB_EHIP, "internal: fused weighted sum timed out");
+    }
     if ((st & 1u) && cxx_index_check)
         return fail(c, HB_EINVAL, "vector::_M_range_check: challenge index out of range");
     for (u32 k = 0; k < ncols; ++k) to_be(&c->hres[(size_t)k * NL], NL, out + (size_t)k * tw, tw);
@@ -1593,6 +1600,80 @@ int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // check_all when the challenge covers every block (:822-827)
     const bool check_all = cxx && chunks >= state_chunks;
     if (check_all) chunks = state_chunks;
+    c->last_launches = 0;
+    if constexpr (NL <= 16) {
+        // One launch (hb_verify_fused_kernel) when the quad engine takes the
+        // challenge, every workgroup's share fits its LDS arena, alpha fits 16
+        // jobs per workgroup and all four keys have the same AES round count;
+        // $HB_NO_VERIFY_FUSE (test switch, A/B): the launch sequence below.
+        const u64 jobs2 = 2 * chunks;
+        if (!cxx && chunks && use_quad(c, jobs2) && !sw_env(c, "HB_NO_VERIFY_FUSE")) {
+            const int G = quad_engine(c, jobs2).grid;
+            const u64 fcmax = (chunks + (u64)G - 1) / (u64)G;
+            u32 off[5];
+            VerifyArgs<NL> V;
+            memset(&V, 0, sizeof V);
+            uint8_t nbe0[8];
+            u64_be(state_chunks, nbe0);
+            int n1 = 0, n2 = 0, n3 = 0, n4 = 0;
+            if (fcmax <= HB_FZ_MAXJOBS && S <= 16ull * (u64)G &&
+                hb_fz_layout((u32)fcmax, NL, 1, 4ull * NL, 8, off) <= HB_FZ_BYTES &&
+                make_prf<2>(chal_key, chal_key_len, nbe0, 8, V.pi, n1) &&
+                make_prf<NL>(chal_key, chal_key_len, vmax_be, vmax_len, V.pv, n2) &&
+                make_prf<NL>(f_key, key_len, p_be, p_len, V.pf, n3) &&
+                make_prf<NL>(a_key, key_len, p_be, p_len, V.pa, n4) && n1 == n2 && n2 == n3 && n3 == n4) {
+                if (c->verify_dirty) {
+                    HB_CHECK(hipMemsetAsync(c->queue + HB_QSLOT * 12, 0, 4 * HB_QSLOT * sizeof(unsigned long long),
+                                            c->stream), "hipMemsetAsync");
+                    if (c->ctl.n) HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync");
+                    if (c->facc.n) HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync");
+                    c->verify_dirty = false;
+                    c->ctl_dirty = false;
+                }
+                if (int rc = ensure_ctl(c, 1)) return rc;
+                const void *was = c->facc.p;
+                HB_CHECK(c->facc.ensure((size_t)NL * 8), "hipMalloc(facc)");
+                if (c->facc.p != was) HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync");
+                if (c->ctl_dirty) {
+                    HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync(ctl)");
+                    HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync(facc)");
+                    c->ctl_dirty = false;
+                }
+                // results, status, token, then mu (read by the kernel from host memory)
+                if (int rc = ensure_hres(c, (size_t)NL + 2 + (size_t)S * NL)) return rc;
+                u32 *hmu = c->hres + NL + 2;
+                for (u32 j = 0; j < S; ++j) {
+                    Limbs m = from_be(mu + (size_t)j * pi.tw, pi.tw, NL);
+                    memcpy(hmu + (size_t)j * NL, m.data(), NL * 4);
+                }
+                make_mod<NL>(p, V.mod);
+                const Limbs &r2 = r2_of(c, p, NL);
+                for (int t = 0; t < NL; ++t) V.r2[t] = r2[t];
+                V.i0 = 0;
+                V.n = chunks;
+                V.ntags = state_chunks;
+                V.S = S;
+                V.fcmax = (u32)fcmax;
+                V.mu = hmu;
+                V.t0 = c->t0;
+                V.queue = c->queue + HB_QSLOT * 12;   // slots 12-15, zero between fused verifies
+                V.flags = flags_word(c);
+                V.qchunk = 16;
+                V.facc = (unsigned long long *)c->facc.p;
+                V.fctl = (unsigned int *)c->ctl.p;
+                V.fout = c->hres;
+                V.ftoken = next_token(c, true);
+                c->sums_in_hres = true;
+                c->sums_polled = true;
+                c->last_launches = 1;
+                c->verify_dirty = true;
+                HB_CHECK(hb_launch_verify_fused<NL>(V, n1, G, c->stream), "hb_verify_fused_kernel launch");
+                const int rc = finish_sums<NL>(c, 1, pi.tw, rhs_out, false);
+                c->verify_dirty = c->ctl_dirty;
+                return rc;
+            }
+        }
+    }
     const int pmode = cxx ? (pi.tw % 16 ? 2 : 1) : 0;
     const int vmode = cxx ? ((bitlen_be(vmax_be, vmax_len) + 7) / 8 % 16 ? 2 : 1) : 0;
     const u64 nterms = chunks + S;

@@ -159,3 +159,59 @@ def test_unplaced_queue_engine_prove_equals_oracle(oracle, monkeypatch):
         monkeypatch.delenv("HB_NO_PROVE_PLACE", raising=False)
         ctx.check(L.hb_device_free(ctx.h, dd))
         ctx.check(L.hb_device_free(ctx.h, dt))
+
+
+# (prime bits, sectors, state chunks (blocks), challenge chunks, key bytes, fused?)
+VERIFY_CASES = [
+    (256, 16, 2 ** 27 + 1, 10000, 32, True),     # configs[4]'s index width and challenge
+    (256, 16, 131073, 12288, 32, True),          # 48 jobs in every workgroup
+    (256, 16, 131073, 12289, 32, False),         # one more: the launch sequence
+    (256, 1, 5, 3, 32, True),                    # tiny: one workgroup pair, alpha of 1 sector
+    (256, 100, 4000, 1000, 32, True),            # alpha over several workgroups (100 > 16)
+    (512, 3, 9000, 4000, 16, True),              # NL = 16, AES-128 keys (NR = 10)
+    (384, 7, 77777, 2500, 24, True),             # NL = 16, AES-192 keys (NR = 12)
+    (1024, 4, 5000, 1000, 32, False),            # NL = 32: the launch sequence
+]
+
+
+@pytest.mark.parametrize("bits,S,nchunks,chunks,klen,fused", VERIFY_CASES)
+def test_fused_verify_equals_launch_sequence_and_oracle(oracle, monkeypatch, bits, S, nchunks, chunks, klen, fused):
+    """PySwizzle.verify's right-hand side sum_i v_i F(idx_i) + sum_j alpha_j
+    mu_j (PySwizzle.py:380-395) from one launch (hb_verify_fused_kernel) and
+    from the launch sequence (HB_NO_VERIFY_FUSE) for an honest mu (the rhs
+    the oracle's verify accepts) and a tampered one (rejected): equal
+    bytes either way."""
+    from heartbeat_amd import _native as nat
+    ctx = nat.context()
+    L = nat.lib()
+    p = _prime(bits)
+    w = nat.width_of(p)
+    rng = random.Random(bits * 1000 + S)
+    fk, ak = bytes(rng.getrandbits(8) for _ in range(klen)), bytes(rng.getrandbits(8) for _ in range(klen))
+    key = bytes(rng.getrandbits(8) for _ in range(32 if klen == 32 else klen))
+    mus = [rng.getrandbits(8 * w) % p for _ in range(S)]
+    pb = nat.be(p)
+    out = {}
+    for off in (False, True):
+        if off:
+            monkeypatch.setenv("HB_NO_VERIFY_FUSE", "1")
+        else:
+            monkeypatch.delenv("HB_NO_VERIFY_FUSE", raising=False)
+        for tamper in (0, 1):
+            m = list(mus)
+            m[0] = (m[0] + tamper) % p
+            mub = b"".join(x.to_bytes(w, "big") for x in m)
+            rhs = ctypes.create_string_buffer(w)
+            ctx.check(L.hb_verify_rhs(ctx.h, pb, len(pb), S, fk, ak, klen, nchunks, key, len(key), chunks, pb,
+                                      len(pb), mub, rhs))
+            ms, nl = ctypes.c_double(), ctypes.c_uint32()
+            ctx.check(L.hb_last_kernel_ms(ctx.h, ctypes.byref(ms), ctypes.byref(nl)))
+            assert nl.value == (1 if fused and not off else 0), (bits, S, chunks, off, nl.value)
+            out[(off, tamper)] = (m, int.from_bytes(rhs.raw, "big"))
+    monkeypatch.delenv("HB_NO_VERIFY_FUSE", raising=False)
+    for tamper in (0, 1):
+        assert out[(False, tamper)] == out[(True, tamper)], (bits, S, chunks, tamper)
+        m, rhs = out[(False, tamper)]
+        # the oracle's verify accepts exactly sigma = rhs
+        assert oracle.verify(p, S, fk, ak, nchunks, key, chunks, p, m, rhs)
+        assert not oracle.verify(p, S, fk, ak, nchunks, key, chunks, p, m, (rhs + 1) % p)
