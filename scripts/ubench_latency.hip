@@ -100,6 +100,31 @@ __device__ __forceinline__ u32 quad_round(const LaneTab &L, u32 w, u32 rk) {
     return hb_xor3(x, qdpp<QP(2, 3, 0, 1)>(c), qdpp<QP(3, 0, 1, 2)>(d));
 }
 
+// variant: the DPP gathers folded into VOP2 XORs (v_xor_b32 with a DPP
+// source): 4 VALU instructions per round instead of 3 DPP moves + 2 XOR3
+template <int CTRL>
+__device__ __forceinline__ u32 xdpp(u32 acc, u32 x) {   // acc ^ x(lane from CTRL)
+    return acc ^ (u32)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ u32 quad_round3(const LaneTab &L, u32 w, u32 rk) {
+    const u32 a = hb_t<0, 0>(L, w), b = hb_t<1, 1>(L, w), c = hb_t<2, 2>(L, w), d = hb_t<3, 3>(L, w);
+    u32 x = a ^ rk;
+    x = xdpp<QP(1, 2, 3, 0)>(x, b);
+    x = xdpp<QP(2, 3, 0, 1)>(x, c);
+    return xdpp<QP(3, 0, 1, 2)>(x, d);
+}
+template <int NR>
+__device__ __forceinline__ void cfb8_step3(const QuadLane &Q, const u32 *rkq, const u32 *rk, u32 &s, u32 pk) {
+    u32 w = s ^ rkq[0];
+    for (int r = 1; r <= NR - 2; ++r) w = quad_round3(Q.L, w, rkq[r]);
+    u32 x = hb_tab_ld(Q.L.tab, hb_perm(w, Q.lbq, Q.selq));
+    x = xdpp<QP(1, 0, 3, 2)>(x, x);
+    x = xdpp<QP(2, 3, 0, 1)>(x ^ rk[4 * (NR - 1)], x);
+    const u32 u = hb_xor3(hb_t<0, 0>(Q.L, x), pk, rk[4 * NR] << 8);
+    const u32 nx = hb_qdpp<HB_QP(1, 2, 3, 0)>(s);
+    s = hb_perm(Q.q3 ? u : nx, s, Q.sels);
+}
+
 // variant: one lookup per lane chain but the three DPP gathers done as
 // one xor tree level (a^b' and c'^d' in parallel)
 __device__ __forceinline__ u32 quad_round2(const LaneTab &L, u32 w, u32 rk) {
@@ -221,6 +246,20 @@ __global__ __launch_bounds__(1024) void k_bench(const u32 *init, u32 *out, unsig
         x = sr;
         break;
     }
+    case 15: {   // quad CFB-8 step with DPP folded into the XORs
+        const QuadLane Q = hb_quad_lane(L);
+        u32 rkv[60], rkq[15];
+        for (int i = 0; i < 60; ++i) rkv[i] = __builtin_amdgcn_readfirstlane(init[200 + i]);
+        const u32 q = lane & 3u;
+        for (int r = 0; r <= 14; ++r) rkq[r] = rkv[4 * r + q];
+        u32 sr = 0;
+        for (int i = 0; i < N_IT / 16; ++i) cfb8_step3<14>(Q, rkq, rkv, sr, y + (u32)i);
+        x = sr;
+        break;
+    }
+    case 16:   // quad round, DPP folded
+        for (int i = 0; i < N_IT; ++i) x = quad_round3(L, x, rk);
+        break;
     case 8:   // 16 independent lookups then xor (lane engine round shape)
         for (int i = 0; i < N_IT; ++i) {
             u32 acc = 0;
@@ -258,9 +297,9 @@ int main() {
     const char *names[] = {"perm+ds_read", "ds_read chase", "mov_dpp+add", "bitop3", "quad_round",
                            "quad_round2", "4 lookups+xor", "ds_bpermute+add", "16 lookups+xor",
                            "quad cfb8 step/16", "cfb8 step2/16", "8x bitop3 /8", "8x perm+read /8",
-                           "8x dpp+add /8", "step -2 rounds/16"};
+                           "8x dpp+add /8", "step -2 rounds/16", "step dppxor/16", "quad_round3"};
     for (int rep = 0; rep < 2; ++rep) {
-        for (int w = 0; w < 15; ++w) {
+        for (int w = 0; w < 17; ++w) {
             hipLaunchKernelGGL(k_bench, dim3(1), dim3(64), 0, 0, init, out, cyc, w);
             unsigned long long c[2];
             hipMemcpy(c, cyc, 16, hipMemcpyDeviceToHost);
@@ -278,6 +317,11 @@ int main() {
         int same = 0;
         for (int i = 0; i < 64; ++i) same += a[i] == b[i];
         printf("step2 registers equal to step: %d of 64 lanes (lane 0: %08x %08x)\n", same, a[0], b[0]);
+        hipLaunchKernelGGL(k_bench, dim3(1), dim3(64), 0, 0, init, out, cyc, 15);
+        hipMemcpy(b, out, sizeof b, hipMemcpyDeviceToHost);
+        same = 0;
+        for (int i = 0; i < 64; ++i) same += a[i] == b[i];
+        printf("dpp-xor step registers equal to step: %d of 64 lanes\n", same);
     }
     // the CFB-8 step with 1..4 waves per SIMD (a workgroup's waves are spread
     // over the CU's four SIMDs)
