@@ -35,37 +35,8 @@ first if the reference's truncation is wanted; INTEGRATION.md section 6.
 import io
 import mmap
 import os
-import queue
-import threading
 
 import numpy as np
-
-# Unmapping a large mapping the encode has read (and page-locked) costs ~1.3 ms
-# per GiB (bench host_path phases: close_ms 5.2 of a 4 GiB file's ~100 ms);
-# mappings of at least this size are closed by a background thread, off the
-# caller's critical path (the pages are not touched after close()).
-BACKGROUND_CLOSE_BYTES = 64 << 20
-_closer = None
-_closer_lock = threading.Lock()
-
-
-def _close_in_background(mm):
-    global _closer
-    with _closer_lock:
-        if _closer is None:
-            q = queue.Queue()
-
-            def run():
-                while True:
-                    m = q.get()
-                    try:
-                        m.close()
-                    except (BufferError, ValueError, OSError):
-                        pass
-
-            threading.Thread(target=run, name="hb-unmap", daemon=True).start()
-            _closer = q
-    _closer.put(mm)
 
 
 class FileBuffer(object):
@@ -156,11 +127,8 @@ class FileBuffer(object):
     def close(self):
         self.arr = None
         if self._mm is not None:
-            mm, self._mm = self._mm, None
-            if len(mm) >= BACKGROUND_CLOSE_BYTES:
-                _close_in_background(mm)
-                return
             try:
-                mm.close()
+                self._mm.close()
             except BufferError:
                 pass
+            self._mm = None

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5: the whole GPU suite, smoke and the default bench line after the
+# fused verify and the background unmap.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r5s}
+mkdir -p $OUT
+step() { local name=$1 limit=$2; shift 2; echo "== $name"; timeout -k 10 $limit "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "   rc=$rc"; tail -1 $OUT/$name.log | cut -c1-200; return $rc; }
+step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider || exit 1
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
+step bench_c3 600 python -u bench.py || exit 1
+echo done
