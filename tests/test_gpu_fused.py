@@ -2,8 +2,8 @@
 in which each workgroup's index waves gather their challenged blocks into LDS,
 its v waves store v R mod p there, and summer waves add the terms as both
 halves arrive; the last workgroup finishes the sums.  Every case is proved
-twice on one context -- fused, and with HB_NO_PROVE_FUSE (PRF launch +
-hb_wsum_kernel) -- and both must equal the oracle.  The launch count tells
+three times on one context -- fused, with HB_NO_PROVE_FUSE (PRF launch +
+hb_wsum_kernel), and fused again -- and each must equal the oracle.  The launch count tells
 which path ran (1 = fused): the cases cover the shapes the host admits (48
 jobs per workgroup and one more, NL = 8 and 16, 16-byte and byte-wise sector
 and tag loads, 2 to 65 columns, empty and ragged files, repeated proves on
