@@ -97,6 +97,9 @@ struct EncodeArgs {
     u32 mfma;
     const u32 *afrag;
     u32 kz[2 * NL + 1];
+    // small inputs (hb_mac_kernel): F(block_base + k), NL limbs per block,
+    // from a quad-engine PRF launch
+    const u32 *fv;
 };
 
 // Prefix image of one PRF key (hb_prefix_kernel).
@@ -117,6 +120,7 @@ struct PrfArgs {
     const u32 *t0;
     unsigned long long *queue;
     u64 qchunk;                   // jobs per queue refill
+    u32 place;                    // quad engine: waves placed by SIMD (hb_prove_place), no queue
 };
 
 template <int NL>

@@ -421,6 +421,23 @@ __global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_ke
     hb_engine<NL, NR>(h, L, A.prf, A.nblocks, A.queue);
 }
 
+// Small inputs (hb_runtime.cpp: as many blocks as the quad engine runs at
+// once): the two-pass engine's fixed costs -- the 2^24-entry prefix image and
+// a retry pass whose lone lanes each run a whole 14-round AES per CFB-8 step
+// -- outweigh its throughput, so F(block_base + k) comes from one quad-engine
+// PRF launch (four lanes per evaluation, every try in one chain) and this
+// kernel adds the sector MAC, one lane per block: tag = F + sum_j alpha_j
+// m_kj mod p (hb_block_tag, the single-pass encode's MAC; PySwizzle.py:297-307).
+template <int NL, int ALIGN>
+__global__ __launch_bounds__(256) void hb_mac_kernel(EncodeArgs<NL> A) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= A.nblocks) return;
+    u32 F[NL], tag[NL];
+    for (int t = 0; t < NL; ++t) F[t] = A.fv[k * NL + t];
+    hb_block_tag<NL, ALIGN>(A.data, A.len, k, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
+    hb_store_tag<NL, ALIGN>(A.tags + k * (u64)A.tw, A.tw, tag);
+}
+
 // The cxx Swizzle encode (shacham_waters_private.cxx:638-702): the same
 // engine and MAC with the cxx prf (CFB-128: nb/16 full AES per try instead of
 // nb byte-0 AES).
@@ -1046,6 +1063,47 @@ struct PrfHandler {
     }
 };
 
+// Static placement of a prove's quad-engine waves (A.place).  The launch
+// lasts as long as its longest v chain, and a wave sharing its SIMD with
+// other busy waves runs its chain up to 1.5x slower (one wave: 1,468 clocks
+// per CFB-8 step; four on one SIMD: up to 2,202, scripts/ubench_latency.hip),
+// so instead of racing for the job queue, each wave is given 16 jobs by
+// position: v waves (nb CFB-8 steps per try) one per SIMD where they fit,
+// index waves (4 steps per try for up to 2^32 tags) on the remaining SIMDs,
+// two or more to a SIMD if they must.  Waves 4m .. 4m+3 of a workgroup run on
+// the CU's four SIMDs (HW_ID, scripts/ubench_hwid.hip): slot s = (w & 3) * G
+// + g is one SIMD and layer w >> 2 a wave on it.  Segregated when the v waves
+// fit one layer and the index waves the free slots' four layers; otherwise
+// balanced: v positions fill slots upward, index positions downward, which
+// stacks at most ceil((nv + ni) / 4G) <= 4 waves on a slot (the host places
+// only when nv + ni <= 16 G).  Returns 1 (v), 2 (index) or 0 (no jobs) and
+// the wave's first job.
+__device__ __forceinline__ int hb_prove_place(u32 G, u32 g, u32 w, u64 n, bool idx_too, u64 &first) {
+    const u64 S4 = 4ull * G, s = (u64)(w & 3u) * G + g, layer = w >> 2;
+    const u64 nv = (n + 15) / 16, ni = idx_too ? nv : 0;
+    const u64 F = nv < S4 ? S4 - nv : 0;
+    if (nv <= S4 && (ni == 0 || ni <= 4 * F)) {
+        if (s < nv) {
+            if (layer != 0) return 0;
+            first = 16 * s;
+            return 1;
+        }
+        const u64 j = layer * F + (s - nv);
+        if (j >= ni) return 0;
+        first = 16 * j;
+        return 2;
+    }
+    const u64 cv = nv / S4 + (s < nv % S4 ? 1u : 0u);
+    if (layer < cv) {
+        first = 16 * (layer * S4 + s);
+        return 1;
+    }
+    const u64 j = (layer - cv) * S4 + (S4 - 1 - s);
+    if (j >= ni) return 0;
+    first = 16 * j;
+    return 2;
+}
+
 // QUAD: one evaluation per four lanes (hb_engine_quad, MODE 0 only) for
 // latency-bound batches.
 template <int NL, int NR, int MODE, bool QUAD = false>
@@ -1054,8 +1112,17 @@ __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prf_kernel(PrfArgs<NL> A) {
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     PrfHandler<NL> h{A};
-    if constexpr (QUAD) hb_engine_quad<NL, NR, PrfHandler<NL>>(h, L, A.prf, A.n, A.queue, A.qchunk);
-    else hb_engine<NL, NR, PrfHandler<NL>, MODE>(h, L, A.prf, A.n, A.queue, A.qchunk);
+    if constexpr (QUAD) {
+        if (A.place) {   // waves placed by SIMD (hb_prove_place), no queue
+            u64 first = 0;
+            if (hb_prove_place(gridDim.x, blockIdx.x, threadIdx.x >> 6, A.n, false, first) == 1)
+                hb_engine_quad<NL, NR, PrfHandler<NL>>(h, L, A.prf, A.n, A.queue, A.qchunk, first);
+            return;
+        }
+        hb_engine_quad<NL, NR, PrfHandler<NL>>(h, L, A.prf, A.n, A.queue, A.qchunk);
+    } else {
+        hb_engine<NL, NR, PrfHandler<NL>, MODE>(h, L, A.prf, A.n, A.queue, A.qchunk);
+    }
 }
 
 // ------------------------------------------------------------------ Montgomery
@@ -1167,46 +1234,6 @@ struct ProveVHandler {
     }
 };
 
-// Static placement of a prove's quad-engine waves (A.place).  The launch
-// lasts as long as its longest v chain, and a wave sharing its SIMD with
-// other busy waves runs its chain up to 1.5x slower (one wave: 1,468 clocks
-// per CFB-8 step; four on one SIMD: up to 2,202, scripts/ubench_latency.hip),
-// so instead of racing for the job queue, each wave is given 16 jobs by
-// position: v waves (nb CFB-8 steps per try) one per SIMD where they fit,
-// index waves (4 steps per try for up to 2^32 tags) on the remaining SIMDs,
-// two or more to a SIMD if they must.  Waves 4m .. 4m+3 of a workgroup run on
-// the CU's four SIMDs (HW_ID, scripts/ubench_hwid.hip): slot s = (w & 3) * G
-// + g is one SIMD and layer w >> 2 a wave on it.  Segregated when the v waves
-// fit one layer and the index waves the free slots' four layers; otherwise
-// balanced: v positions fill slots upward, index positions downward, which
-// stacks at most ceil((nv + ni) / 4G) <= 4 waves on a slot (the host places
-// only when nv + ni <= 16 G).  Returns 1 (v), 2 (index) or 0 (no jobs) and
-// the wave's first job.
-__device__ __forceinline__ int hb_prove_place(u32 G, u32 g, u32 w, u64 n, bool idx_too, u64 &first) {
-    const u64 S4 = 4ull * G, s = (u64)(w & 3u) * G + g, layer = w >> 2;
-    const u64 nv = (n + 15) / 16, ni = idx_too ? nv : 0;
-    const u64 F = nv < S4 ? S4 - nv : 0;
-    if (nv <= S4 && (ni == 0 || ni <= 4 * F)) {
-        if (s < nv) {
-            if (layer != 0) return 0;
-            first = 16 * s;
-            return 1;
-        }
-        const u64 j = layer * F + (s - nv);
-        if (j >= ni) return 0;
-        first = 16 * j;
-        return 2;
-    }
-    const u64 cv = nv / S4 + (s < nv % S4 ? 1u : 0u);
-    if (layer < cv) {
-        first = 16 * (layer * S4 + s);
-        return 1;
-    }
-    const u64 j = (layer - cv) * S4 + (S4 - 1 - s);
-    if (j >= ni) return 0;
-    first = 16 * j;
-    return 2;
-}
 
 // ------------------------------------------------------------------ fused prove
 // One launch for the whole PySwizzle prove of a device-resident file when
@@ -1896,6 +1923,14 @@ hipError_t hb_launch_encode_pass(const EncodeArgs<NL> &A, int nr, int align, int
     return hipGetLastError();
 }
 
+template <int NL>
+hipError_t hb_launch_mac(const EncodeArgs<NL> &A, int align, hipStream_t s) {
+    const u64 grid = (A.nblocks + 255) / 256;
+    if (align == 16) HB_LAUNCH((hb_mac_kernel<NL, 16>), dim3((u32)grid), dim3(256), s, A);
+    else HB_LAUNCH((hb_mac_kernel<NL, 1>), dim3((u32)grid), dim3(256), s, A);
+    return hipGetLastError();
+}
+
 // One launcher per pass (hb_launch_encode_pass), so that the wide-limb
 // kernels of each pass can be instantiated in a translation unit of their own
 // (HB_INST_ENC_PASS) and built in parallel.
@@ -1982,7 +2017,8 @@ hipError_t hb_launch_verify_fused(const VerifyArgs<NL> &A, int nr, int grid, hip
 // halves can go to separate translation units (parallel builds of the
 // slow-to-compile wide-limb kernels).
 #define HB_INST_ENC(NL) \
-    template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t);
+    template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t); \
+    template hipError_t hb_launch_mac<NL>(const EncodeArgs<NL> &, int, hipStream_t);
 // the encode dispatcher alone, its passes instantiated elsewhere
 #define HB_EXTERN_ENC_PASSES(NL)                                                                  \
     extern template hipError_t hb_launch_encode_pass<NL, 0>(const EncodeArgs<NL> &, int, int, int, hipStream_t); \

@@ -31,6 +31,7 @@ using namespace hbhost;
 
 // launchers (hb_kernels.hip)
 template <int NL> hipError_t hb_launch_encode(const EncodeArgs<NL> &, int, int, int, int, hipStream_t);
+template <int NL> hipError_t hb_launch_mac(const EncodeArgs<NL> &, int, hipStream_t);
 hipError_t hb_launch_prefix(const PrefixArgs &, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_prf(const PrfArgs<NL> &, int, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_mont(const MontArgs<NL> &, hipStream_t);
@@ -193,6 +194,7 @@ const SwitchName kSwitches[] = {
     {"HB_NO_PROVE_FUSE", HB_SW_NO_PROVE_FUSE},
     {"HB_SYNC_WAIT", HB_SW_SYNC_WAIT},
     {"HB_NO_VERIFY_FUSE", HB_SW_NO_VERIFY_FUSE},
+    {"HB_NO_SMALL_ENCODE", HB_SW_NO_SMALL_ENCODE},
 };
 
 int nl_for_bits(int bits) {
@@ -304,6 +306,9 @@ int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_
     const bool quad = mode == 0 && use_quad(c, n);
     const EngineShape es = quad ? quad_engine(c, n) : small_engine(c, n);
     A.qchunk = es.chunk;
+    // quad waves placed by SIMD as in the prove (hb_prove_place; every quad
+    // launch's waves fit: use_quad); $HB_NO_PROVE_PLACE: the job-queue race
+    A.place = quad && !sw_env(c, "HB_NO_PROVE_PLACE") ? 1u : 0u;
     HB_CHECK(hipMemsetAsync(A.queue, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
     HB_CHECK(hb_launch_prf<NL>(A, nr, quad ? 3 : mode, es.grid, c->stream), "hb_prf_kernel launch");
     return 0;
@@ -377,9 +382,15 @@ void prepare_nl(hb_ctx *c) {
     memset(&E, 0, sizeof E);
     for (int pass = 0; pass <= 3; ++pass)
         for (int align : {16, 1}) (void)hb_launch_encode<NL>(E, 14, align, pass, 0, c->stream);
+    for (int align : {16, 1}) (void)hb_launch_mac<NL>(E, align, c->stream);
     PrfArgs<NL> P;
     memset(&P, 0, sizeof P);
     for (int mode : {0, 3}) (void)hb_launch_prf<NL>(P, 14, mode, 0, c->stream);
+    if constexpr (NL <= 16) {
+        VerifyArgs<NL> VA;
+        memset(&VA, 0, sizeof VA);
+        (void)hb_launch_verify_fused<NL>(VA, 14, 0, c->stream);
+    }
     MontArgs<NL> M;
     memset(&M, 0, sizeof M);
     (void)hb_launch_mont<NL>(M, c->stream);   // n = 0: grid 0
@@ -894,6 +905,14 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 
     EncodeArgs<NL> A;
     memset(&A, 0, sizeof A);
+    // Small inputs -- as many blocks per launch as the quad engine runs at once
+    // (use_quad): F from one placed quad-engine PRF launch + hb_mac_kernel,
+    // no prefix image and no retry pass ($HB_NO_SMALL_ENCODE, test switch:
+    // the two-pass engine for every size).
+    const u64 cb0 = C ? ((256ull << 20) / C ? (256ull << 20) / C : 1) : 1;
+    const u64 launch_max = (flags & HB_DATA_ON_DEVICE) ? nblocks : (nblocks < cb0 ? nblocks : cb0);
+    const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max && use_quad(c, launch_max) &&
+                       !sw_env(c, "HB_NO_SMALL_ENCODE");
     int mf_layout = 0;   // MFMA MAC table layout (0: VALU MAC)
     if constexpr (NL == 8) {
         // MFMA MAC tables (hb_mfma_block_acc): 256-bit primes with whole
@@ -905,7 +924,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         // read per call like every switch)
         const char *ms = sw_env(c, "HB_MFMA_MIN_S");
         const u32 min_s = ms ? (u32)atoi(ms) : 4u;
-        if (!cxx && pi.ss == 32 && S >= min_s && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
+        if (!cxx && !small && pi.ss == 32 && S >= min_s && S <= HB_MFMA_MAX_S && !(flags & HB_ENCODE_SINGLE_PASS) &&
             !sw_env(c, "HB_NO_MFMA")) {
             // 3: the 16x16x64 MFMA, whose B operand is the whole-line load
             // shape (S even); 2: 32x32x32 with whole-line loads and an
@@ -957,7 +976,11 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // PySwizzle; the cxx prf (2 AES per try, no prefix) runs single-pass: a
     // cxx two-pass variant with the MFMA MAC measured 1,799 vs 2,246 GiB/s
     // (profiles/r02/s8)
-    const bool two_pass = !cxx && A.prf.nb >= 4 && !(flags & HB_ENCODE_SINGLE_PASS);
+    const bool two_pass = !cxx && !small && A.prf.nb >= 4 && !(flags & HB_ENCODE_SINGLE_PASS);
+    if (small) {
+        HB_CHECK(c->vals.ensure((size_t)launch_blocks * NL * 4), "hipMalloc(F)");
+        A.fv = (const u32 *)c->vals.p;
+    }
     if (two_pass) {
         A.retry_cap = retry_capacity(c, p_be, p_len, launch_blocks);
         HB_CHECK(c->retry.ensure((size_t)(A.retry_cap ? A.retry_cap : 1) * sizeof(HbRetry)), "hipMalloc(retry)");
@@ -1009,6 +1032,25 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         A.block_base = base;
         A.tags = tg;
         const int align = full16(pi, NL, C, d) ? 16 : 1;
+        if (small) {
+            // F(base + k): placed quad waves, queue slot 0 not cleared per
+            // chunk (no job counter; tries and abandoned jobs add up)
+            PrfArgs<NL> F;
+            memset(&F, 0, sizeof F);
+            F.prf = A.prf;
+            F.x0 = base;
+            F.n = nb;
+            F.out = (u32 *)c->vals.p;
+            F.t0 = c->t0;
+            F.queue = q0;
+            const EngineShape es = quad_engine(c, nb);
+            F.qchunk = es.chunk;
+            F.place = 1;
+            HB_CHECK(hb_launch_prf<NL>(F, nr, 3, es.grid, c->stream), "hb_prf_kernel launch");
+            HB_CHECK(hb_launch_mac<NL>(A, align, c->stream), "hb_mac_kernel launch");
+            c->last_launches += 2;
+            return 0;
+        }
         // queue[0] is the per-launch job counter (and queue[3] the retry
         // count); queue[1] accumulates tries
         HB_CHECK(hipMemsetAsync(q0, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
@@ -1117,12 +1159,16 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     c->last_ms = ms_total;
     if (!tags_dev && data_dev)
         HB_CHECK(hipMemcpy(tags, dtags, (size_t)(nblocks * pi.tw), hipMemcpyDeviceToHost), "hipMemcpy(tags)");
-    unsigned long long q[HB_QSLOT], r[HB_QSLOT];
-    HB_CHECK(hipMemcpy(q, q0, sizeof q, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
-    HB_CHECK(hipMemcpy(r, q7, sizeof r, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
+    // every engine slot in one read: the encode's (0: first pass or the small
+    // path's PRF, 7: retry pass) and any other launch's abandoned jobs
+    unsigned long long qs[16 * HB_QSLOT];
+    HB_CHECK(hipMemcpy(qs, c->queue, sizeof qs, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
+    const unsigned long long *q = qs, *r = qs + HB_QSLOT * HB_SLOT_RETRY;
     if (q[2] || r[2]) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate for some blocks");
     if (tries_out) *tries_out = q[1] + r[1];
-    return check_prf_slots(c);
+    for (int s = 0; s < 16; ++s)
+        if (qs[s * HB_QSLOT + 2]) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate");
+    return 0;
 }
 
 // ------------------------------------------------------------------ sums
@@ -1277,7 +1323,10 @@ struct Gather {
     // gather is random reads of a (mapped) file, bound by page-cache / DRAM
     // latency per block, so it scales with threads.
     void run_parallel(const u64 *idx, u64 n, uint8_t *blocks, uint8_t *gtags, int threads) const {
-        const u64 T = threads < 2 || n < 2048 ? 1 : (u64)threads;
+        // about 1,024 blocks per thread at least: a thread's start costs
+        // ~20 us, the gather of a block well under 1 us
+        u64 T = threads < 2 ? 1 : (u64)threads;
+        if (T > n / 1024) T = n / 1024 ? n / 1024 : 1;
         if (T == 1) return run(idx, n, blocks, gtags);
         std::vector<std::thread> ts;
         for (u64 t = 0; t < T; ++t) {

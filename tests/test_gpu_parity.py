@@ -93,8 +93,14 @@ def test_encode_golden_host_path(golden_encode, pys):
         assert tag.sigma == [int(t, 16) for t in c["tags"]], c["name"]
 
 
+@pytest.mark.parametrize("engine", ["small", "two_pass"])
 @pytest.mark.parametrize("misalign", [0, 1])
-def test_encode_golden_device_path(golden_encode, nat, misalign):
+def test_encode_golden_device_path(golden_encode, nat, misalign, engine, monkeypatch):
+    """Every golden case through the C ABI from device memory, on the
+    small-input path (placed quad PRF + hb_mac_kernel, the default for these
+    sizes) and on the two-pass engine (HB_NO_SMALL_ENCODE)."""
+    if engine == "two_pass":
+        monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")
     for c in golden_encode["cases"]:
         p = int(c["prime"], 16)
         w = nat.width_of(p)
@@ -279,7 +285,7 @@ def test_device_resident_64mib_vs_oracle(nat, oracle, S, prime_name):
 
 @pytest.mark.parametrize("prime_name", ["p256", "p256max", "p256lo"])
 @pytest.mark.parametrize("S", [4, 6, 17, 20, 36])
-def test_mfma_mac_sector_counts_vs_oracle(nat, oracle, S, prime_name):
+def test_mfma_mac_sector_counts_vs_oracle(nat, oracle, S, prime_name, monkeypatch):
     """The first pass's MFMA MAC (hb_mfma_block_acc, dense digit tiles from
     mfma_tables) at the sector counts the 64 MiB test does not reach: S = 4
     (the smallest MFMA case), 6 and 17 (sector-shaped loads, S % 4 != 0),
@@ -288,6 +294,7 @@ def test_mfma_mac_sector_counts_vs_oracle(nat, oracle, S, prime_name):
     (p256lo, half the first tries rejected) and just below 2^256 (p256max: the
     digit representatives r - p at the edge of their range).  A ragged 2 MiB
     device-resident file, block_base != 0; every tag == the oracle."""
+    monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")   # the two-pass engine at this size
     primes = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))
     p = int(primes[prime_name], 16)
     L = (2 << 20) + 777
@@ -318,6 +325,7 @@ def test_mfma_selectable_layouts_vs_oracle(nat, oracle, monkeypatch, switch, S):
     1, here at even S, which the default build gives the 16x16x64 MAC).
     Primes just below 2^256 (digit representatives at the edge of their range)
     and p256; a ragged 2 MiB device-resident file; every tag == the oracle."""
+    monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")   # the two-pass engine at this size
     primes = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))
     monkeypatch.setenv(switch, "1")
     L = (2 << 20) + 333
@@ -343,10 +351,12 @@ def test_mfma_selectable_layouts_vs_oracle(nat, oracle, monkeypatch, switch, S):
 
 @pytest.mark.parametrize("S,prime_name", [(16, "p256"), (1, "p256"), (5, "p255"), (16, "p256lo"),
                                           (3, "p1024"), (4, "p61")])
-def test_two_pass_equals_single_pass(nat, S, prime_name):
-    """The two-pass encode (prefix image first pass + retry list) == the
-    single-pass engine (HB_ENCODE_SINGLE_PASS), 16 MiB device-resident; p256lo
-    (2^255 < p) rejects half the first tries."""
+def test_two_pass_equals_single_pass(nat, S, prime_name, monkeypatch):
+    """The two-pass encode (prefix image first pass + retry list, forced with
+    HB_NO_SMALL_ENCODE where the input is small) == the single-pass engine
+    (HB_ENCODE_SINGLE_PASS) == the small-input path (placed quad PRF +
+    hb_mac_kernel, the default below 65,537 blocks), 16 MiB device-resident;
+    p256lo (2^255 < p) rejects half the first tries."""
     primes = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))
     p = int(primes[prime_name], 16)
     w = nat.width_of(p)
@@ -356,29 +366,36 @@ def test_two_pass_equals_single_pass(nat, S, prime_name):
     buf = DevBuf(nat, L)
     t1 = DevBuf(nat, nb * w)
     t2 = DevBuf(nat, nb * w)
+    t3 = DevBuf(nat, nb * w)
     try:
         ctx = nat.context()
         ctx.check(nat.lib().hb_fill_random(ctx.h, buf.p, L, 4242))
         fk, ak = hashlib.sha256(b"tp-f").digest(), hashlib.sha256(b"tp-a").digest()
         pb = nat.be(p)
         tries = []
-        for flags, tb in ((3, t1), (3 | nat.HB_ENCODE_SINGLE_PASS, t2)):
+        for flags, tb, two_pass in ((3, t1, True), (3 | nat.HB_ENCODE_SINGLE_PASS, t2, False), (3, t3, False)):
+            if two_pass:
+                monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")
+            else:
+                monkeypatch.delenv("HB_NO_SMALL_ENCODE", raising=False)
             tr = ctypes.c_uint64()
             ctx.check(nat.lib().hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, buf.p, L, nb, tb.p,
                                           flags, ctypes.byref(tr)))
             tries.append(tr.value)
-        assert t1.download() == t2.download()
+        assert t1.download() == t2.download() == t3.download()
         # same PRF streams: the same number of tries either way
-        assert tries[0] == tries[1]
+        assert tries[0] == tries[1] == tries[2]
     finally:
         buf.free()
         t1.free()
         t2.free()
+        t3.free()
 
 
 def test_two_pass_retry_list_overflow(nat, monkeypatch):
     """A retry list too small for the rejected first tries: the first pass
     finishes the overflow in place, tags unchanged."""
+    monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")   # the two-pass engine at this size
     p = int(json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))["p256lo"], 16)
     S, L = 4, 4 << 20
     nb = L // (32 * S) + 1
@@ -404,6 +421,7 @@ def test_retry_list_late_entries(nat, oracle, monkeypatch):
     rejections, forced for all of them by HB_TEST_NO_EARLY_LIST) are hashed by
     the retry pass: tags == the default path (early entries with digests) ==
     the oracle, with a full and an overflowing retry list."""
+    monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")   # the two-pass engine at this size
     p = int(json.load(open(os.path.join(os.path.dirname(__file__), "golden", "primes.json")))["p256"], 16)
     S, L = 16, 6 << 20
     nb = L // (32 * S) + 1
@@ -670,3 +688,53 @@ def test_prove_mixed_residency_equals_device(nat, oracle):
     finally:
         buf.free()
         tb.free()
+
+
+@pytest.mark.parametrize("bits,S,nbytes", [
+    (1024, 10, 1 << 20),                    # PySwizzle's defaults on a 1 MiB file
+    (256, 16, 65535 * 512),                 # 65,536 blocks: the largest small input (256 CUs)
+    (256, 16, 65536 * 512),                 # one block more: the two-pass engine
+    (256, 1, (3 << 20) + 7),                # S = 1, ragged tail
+    (384, 3, 200000),                       # 48-byte sectors: byte-wise MAC loads
+])
+def test_small_encode_equals_two_pass_and_oracle(nat, oracle, monkeypatch, bits, S, nbytes):
+    """Small inputs take the quad-PRF + hb_mac_kernel path; the same encode
+    forced through the two-pass engine (HB_NO_SMALL_ENCODE) and the oracle
+    agree, from device memory and from host memory through the drop-in API.
+    Reference: PySwizzle.py:279-314."""
+    import random
+    pys = importlib.import_module("heartbeat_amd.PySwizzle.PySwizzle")
+    rng = random.Random(bits * 31 + S)
+    while True:
+        p = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        if pys._is_probable_prime(p):
+            break
+    w = nat.width_of(p)
+    C = (p.bit_length() // 8) * S
+    nb = nbytes // C + 1
+    data = np.random.default_rng(bits + S).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+    fk, ak = hashlib.sha256(b"se-f%d" % bits).digest(), hashlib.sha256(b"se-a%d" % bits).digest()
+    buf = DevBuf(nat, nbytes)
+    res = []
+    try:
+        buf.upload(data)
+        for two_pass in (False, True):
+            if two_pass:
+                monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")
+            else:
+                monkeypatch.delenv("HB_NO_SMALL_ENCODE", raising=False)
+            tb = DevBuf(nat, nb * w)
+            try:
+                dev_encode(nat, p, S, fk, ak, buf.p, nbytes, nb, tb.p)
+                res.append(tb.download())
+            finally:
+                tb.free()
+            tag, n = pys.encode_file(p, S, fk, ak, io.BytesIO(data))
+            assert n == nb and bytes(tag.raw(p)) == res[-1]
+    finally:
+        monkeypatch.delenv("HB_NO_SMALL_ENCODE", raising=False)
+        buf.free()
+    assert res[0] == res[1]
+    want = oracle.encode(p, S, fk, ak, data, nthreads=8) if nb <= 70000 else None
+    if want is not None:
+        assert split_tags(res[0], w) == want
