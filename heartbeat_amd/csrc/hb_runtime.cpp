@@ -103,6 +103,7 @@ struct hb_ctx {
     DevBuf mseeds, moffs, mdig;   // Merkle chunk seeds, offsets, HMAC digests
     DevBuf gdev;         // device-resident prove: the challenged blocks and tags, gathered
     DevBuf facc;         // fused prove: per-column limb sums over workgroups (zero between operations)
+    DevBuf gup;          // prove of a small host file: the file, uploaded whole
     HostBuf gstage[2];   // host-file prove: pinned gather buffers (blocks | tags), double-buffered
     HostBuf hscratch;    // pinned staging of the encode's small host round trips (alpha, MFMA tables)
     // the alpha D2H into hscratch done / the MFMA-table H2D out of it done
@@ -195,6 +196,7 @@ const SwitchName kSwitches[] = {
     {"HB_SYNC_WAIT", HB_SW_SYNC_WAIT},
     {"HB_NO_VERIFY_FUSE", HB_SW_NO_VERIFY_FUSE},
     {"HB_NO_SMALL_ENCODE", HB_SW_NO_SMALL_ENCODE},
+    {"HB_NO_PROVE_UPLOAD", HB_SW_NO_PROVE_UPLOAD},
 };
 
 int nl_for_bits(int bits) {
@@ -1432,8 +1434,23 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     const bool quad = !cxx && use_quad(c, 2 * n);
     const EngineShape es = quad ? quad_engine(c, 2 * n) : small_engine(c, 2 * n);
     PA.qchunk = es.chunk;
-    const bool data_dev = flags & HB_DATA_ON_DEVICE;
+    bool data_dev = flags & HB_DATA_ON_DEVICE;
     bool tags_dev = flags & HB_TAGS_ON_DEVICE;
+    // A host file that is small next to what the host gather would move (at
+    // most twice its bytes, or 8 MiB) and fits a 4 GiB staging buffer goes
+    // to the device whole -- one sequential H2D -- and is proved
+    // device-resident (the fused launch where it applies), instead of a D2H
+    // of the indices, a host gather of n random blocks and an H2D between
+    // two launches.  $HB_NO_PROVE_UPLOAD and $HB_TEST_PROVE_BATCH (test
+    // switches): the host gather.
+    const u64 up_max = 2 * n * C > (8ull << 20) ? 2 * n * C : (8ull << 20);
+    if (!data_dev && !cxx && !check_all && len <= up_max && len <= (4ull << 30) &&
+        !sw_env(c, "HB_NO_PROVE_UPLOAD") && !sw_env(c, "HB_TEST_PROVE_BATCH")) {
+        HB_CHECK(c->gup.ensure((size_t)(len ? len : 16)), "hipMalloc(file)");
+        if (len) HB_CHECK(hipMemcpyAsync(c->gup.p, data, (size_t)len, hipMemcpyHostToDevice, c->stream), "H2D(file)");
+        data = (const uint8_t *)c->gup.p;
+        data_dev = true;
+    }
     if (data_dev && !tags_dev) {
         // device-resident file, host tags: upload the tags (1/S of the file's
         // size at most) and gather on the device, instead of copying the
@@ -1884,7 +1901,7 @@ void hb_ctx_destroy(hb_ctx *c) {
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
                       &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
                       &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig, &c->gdev,
-                      &c->facc};
+                      &c->facc, &c->gup};
     for (DevBuf *b : bufs) b->release();
     if (c->hres) (void)hipHostFree(c->hres);
     c->gstage[0].release();

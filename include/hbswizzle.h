@@ -120,6 +120,7 @@ const char *hb_build_flags_string(void);
 #define HB_SW_SYNC_WAIT 16384u       /* HB_SYNC_WAIT: a fused prove waits for its stream instead of polling its token */
 #define HB_SW_NO_VERIFY_FUSE 32768u  /* HB_NO_VERIFY_FUSE: verify as a launch sequence (PRFs, mont, hb_wsum_kernel) */
 #define HB_SW_NO_SMALL_ENCODE 65536u /* HB_NO_SMALL_ENCODE: the two-pass engine for small inputs too */
+#define HB_SW_NO_PROVE_UPLOAD 131072u /* HB_NO_PROVE_UPLOAD: small host files are gathered on the host, not uploaded */
 uint32_t hb_test_switches(void);
 
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens

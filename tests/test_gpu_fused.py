@@ -215,3 +215,49 @@ def test_fused_verify_equals_launch_sequence_and_oracle(oracle, monkeypatch, bit
         # the oracle's verify accepts exactly sigma = rhs
         assert oracle.verify(p, S, fk, ak, nchunks, key, chunks, p, m, rhs)
         assert not oracle.verify(p, S, fk, ak, nchunks, key, chunks, p, m, (rhs + 1) % p)
+
+
+@pytest.mark.parametrize("bits,S,nbytes,chunks,uploaded", [
+    (256, 16, 1 << 20, 2049, True),             # a 1 MiB file and its default challenge: uploaded, fused
+    (1024, 10, 1 << 20, 820, True),             # PySwizzle's defaults: uploaded, two launches (NL = 32)
+    (256, 1, (5 << 20) + 3, 3000, True),        # under 8 MiB: uploaded
+    (256, 16, 16 << 20, 10000, False),          # 16 MiB > 2 x 5.1 MB of challenged blocks: host gather
+])
+def test_host_prove_upload_equals_gather_and_oracle(oracle, monkeypatch, bits, S, nbytes, chunks, uploaded):
+    """A prove of a host file small next to its challenge uploads the file
+    and proves it device-resident; with HB_NO_PROVE_UPLOAD the challenged
+    blocks are gathered on the host.  Both == the oracle, through the C ABI
+    from host memory (PySwizzle.py:333-370)."""
+    from heartbeat_amd import _native as nat
+    ctx = nat.context()
+    L = nat.lib()
+    p = _prime(bits)
+    w = nat.width_of(p)
+    data = np.random.default_rng(bits + nbytes).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+    fk, ak = hashlib.sha256(b"up-f%d" % bits).digest(), hashlib.sha256(b"up-a%d" % bits).digest()
+    tags = oracle.encode(p, S, fk, ak, data, nthreads=8)
+    traw = b"".join(t.to_bytes(w, "big") for t in tags)
+    key = hashlib.sha256(b"up-c%d" % nbytes).digest()
+    want = oracle.prove(p, S, key, chunks, p, tags, data)
+    pb = nat.be(p)
+    dbuf = ctypes.create_string_buffer(data, max(nbytes, 1))
+    tbuf = ctypes.create_string_buffer(traw, len(traw))
+    launches = []
+    try:
+        for off in (False, True):
+            if off:
+                monkeypatch.setenv("HB_NO_PROVE_UPLOAD", "1")
+            else:
+                monkeypatch.delenv("HB_NO_PROVE_UPLOAD", raising=False)
+            mu = ctypes.create_string_buffer(w * S)
+            sg = ctypes.create_string_buffer(w)
+            ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, key, 32, chunks, pb, len(pb), tbuf, len(tags), dbuf, nbytes,
+                                 0, mu, sg))
+            ms, nl = ctypes.c_double(), ctypes.c_uint32()
+            ctx.check(L.hb_last_kernel_ms(ctx.h, ctypes.byref(ms), ctypes.byref(nl)))
+            launches.append(nl.value)
+            assert (_ints(mu.raw, w, S), int.from_bytes(sg.raw, "big")) == want, (bits, S, nbytes, off)
+    finally:
+        monkeypatch.delenv("HB_NO_PROVE_UPLOAD", raising=False)
+    if uploaded and bits <= 512:
+        assert launches[0] == 1      # the fused launch on the uploaded file

@@ -615,7 +615,10 @@ def test_prove_host_file_multi_batch(nat, oracle, monkeypatch):
     challenge runs 4 batches (3 of them gathered on 4 threads); a 255-bit prime
     (31-byte sectors, 10 per block: C = 310) puts each batch's tag region at an
     unaligned offset of its staging buffer.  == the oracle and == the same
-    proof with everything device-resident.  Reference: PySwizzle.py:351-368."""
+    proof with everything device-resident.  (The hook also keeps the 3 MiB
+    file from being uploaded whole; the last run, without it, uploads it --
+    a small host file is proved device-resident)
+    Reference: PySwizzle.py:351-368."""
     from conftest import load_golden
     p = int(load_golden("primes.json")["p255"], 16)
     S, ss = 10, 31
