@@ -123,6 +123,19 @@ struct PrfArgs {
     u32 place;                    // quad engine: waves placed by SIMD (hb_prove_place), no queue
 };
 
+// Small-input encode (hb_prf_pair_kernel): F(x0 + k) for the blocks (f) and
+// alpha_j R mod p for the sectors in ONE launch (PySwizzle.py:291, 302).
+template <int NL>
+struct Prf2Args {
+    PrfArgs<NL> f;
+    PrfParams<NL> pa;             // alpha = KeyedPRF(alpha_key, p)
+    ModP<NL> mod;
+    u32 r2[NL];                   // R^2 mod p
+    u64 S;
+    u32 *amont;                   // S x NL limbs: alpha_j R mod p
+    unsigned long long *aqueue;   // alpha's engine slot
+};
+
 template <int NL>
 struct MontArgs {
     ModP<NL> mod;

@@ -1125,6 +1125,41 @@ __global__ __launch_bounds__(HB_ENGINE_WG) void hb_prf_kernel(PrfArgs<NL> A) {
     }
 }
 
+// alpha_j R mod p (PySwizzle.py:291, 302), written in Montgomery form.
+template <int NL>
+struct AlphaMontHandler {
+    const Prf2Args<NL> &A;
+    __device__ __forceinline__ u64 x_of(u64 job) const { return job; }
+    __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
+    __device__ __forceinline__ void fail(u64) const {}
+    __device__ __forceinline__ void accept(u64 job, const u32 a[NL]) const {
+        u32 y[NL];
+        hb_to_mont<NL>(a, A.r2, A.mod, y);
+        for (int t = 0; t < NL; ++t) A.amont[job * NL + t] = y[t];
+    }
+};
+
+// The small-input encode's PRFs in one launch: placed quad waves (position
+// p = (w >> 2) 4G + (w & 3) G + g, one wave per SIMD first), the blocks'
+// F(x0 + k) on positions [0, nf) and the sectors' alpha_j on the next ones, so
+// the alpha chains run beside the F chains instead of before them.
+template <int NL, int NR>
+__global__ __launch_bounds__(HB_ENGINE_WG) void hb_prf_pair_kernel(Prf2Args<NL> A) {
+    __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
+    hb_fill_lds(lds, A.f.t0);
+    const LaneTab L = hb_lane_tab(lds);
+    const u64 G = gridDim.x, w = threadIdx.x >> 6;
+    const u64 pos = (w >> 2) * 4 * G + (w & 3) * G + blockIdx.x;
+    const u64 nf = (A.f.n + 15) / 16, na = (A.S + 15) / 16;
+    if (pos < nf) {
+        PrfHandler<NL> h{A.f};
+        hb_engine_quad<NL, NR, PrfHandler<NL>>(h, L, A.f.prf, A.f.n, A.f.queue, A.f.qchunk, 16 * pos);
+    } else if (pos < nf + na) {
+        AlphaMontHandler<NL> h{A};
+        hb_engine_quad<NL, NR, AlphaMontHandler<NL>>(h, L, A.pa, A.S, A.aqueue, A.f.qchunk, 16 * (pos - nf));
+    }
+}
+
 // ------------------------------------------------------------------ Montgomery
 template <int NL>
 __global__ __launch_bounds__(256) void hb_mont_kernel(MontArgs<NL> A) {
@@ -1924,6 +1959,15 @@ hipError_t hb_launch_encode_pass(const EncodeArgs<NL> &A, int nr, int align, int
 }
 
 template <int NL>
+hipError_t hb_launch_prf_pair(const Prf2Args<NL> &A, int nr, int grid, hipStream_t s) {
+    dim3 g(grid), b(HB_ENGINE_WG);
+    if (nr == 14) HB_LAUNCH((hb_prf_pair_kernel<NL, 14>), g, b, s, A);
+    else if (nr == 12) HB_LAUNCH((hb_prf_pair_kernel<NL, 12>), g, b, s, A);
+    else HB_LAUNCH((hb_prf_pair_kernel<NL, 10>), g, b, s, A);
+    return hipGetLastError();
+}
+
+template <int NL>
 hipError_t hb_launch_mac(const EncodeArgs<NL> &A, int align, hipStream_t s) {
     const u64 grid = (A.nblocks + 255) / 256;
     if (align == 16) HB_LAUNCH((hb_mac_kernel<NL, 16>), dim3((u32)grid), dim3(256), s, A);
@@ -2018,7 +2062,8 @@ hipError_t hb_launch_verify_fused(const VerifyArgs<NL> &A, int nr, int grid, hip
 // slow-to-compile wide-limb kernels).
 #define HB_INST_ENC(NL) \
     template hipError_t hb_launch_encode<NL>(const EncodeArgs<NL> &, int, int, int, int, hipStream_t); \
-    template hipError_t hb_launch_mac<NL>(const EncodeArgs<NL> &, int, hipStream_t);
+    template hipError_t hb_launch_mac<NL>(const EncodeArgs<NL> &, int, hipStream_t); \
+    template hipError_t hb_launch_prf_pair<NL>(const Prf2Args<NL> &, int, int, hipStream_t);
 // the encode dispatcher alone, its passes instantiated elsewhere
 #define HB_EXTERN_ENC_PASSES(NL)                                                                  \
     extern template hipError_t hb_launch_encode_pass<NL, 0>(const EncodeArgs<NL> &, int, int, int, hipStream_t); \

@@ -32,6 +32,7 @@ using namespace hbhost;
 // launchers (hb_kernels.hip)
 template <int NL> hipError_t hb_launch_encode(const EncodeArgs<NL> &, int, int, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_mac(const EncodeArgs<NL> &, int, hipStream_t);
+template <int NL> hipError_t hb_launch_prf_pair(const Prf2Args<NL> &, int, int, hipStream_t);
 hipError_t hb_launch_prefix(const PrefixArgs &, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_prf(const PrfArgs<NL> &, int, int, int, hipStream_t);
 template <int NL> hipError_t hb_launch_mont(const MontArgs<NL> &, hipStream_t);
@@ -385,6 +386,9 @@ void prepare_nl(hb_ctx *c) {
     for (int pass = 0; pass <= 3; ++pass)
         for (int align : {16, 1}) (void)hb_launch_encode<NL>(E, 14, align, pass, 0, c->stream);
     for (int align : {16, 1}) (void)hb_launch_mac<NL>(E, align, c->stream);
+    Prf2Args<NL> P2;
+    memset(&P2, 0, sizeof P2);
+    (void)hb_launch_prf_pair<NL>(P2, 14, 0, c->stream);
     PrfArgs<NL> P;
     memset(&P, 0, sizeof P);
     for (int mode : {0, 3}) (void)hb_launch_prf<NL>(P, 14, mode, 0, c->stream);
@@ -898,23 +902,27 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     const bool cxx = flags & HB_PRF_CXX;
     if (cxx && (pi.tw % 16 != 0 || pi.tw > 4u * NL))
         return fail(c, HB_EUNSUPPORTED, "cxx prf mode needs ByteCount(p) to be a multiple of 16");
-    int rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, cxx ? 1 : 0);
-    if (rc) return rc;
-    mark("alpha PRF");
-    rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S);
-    if (rc) return rc;
-    mark("alpha PRF + Montgomery");
+    // Small inputs -- as many blocks per launch as the quad engine runs at once
+    // (use_quad): one placed quad-engine launch for the blocks' F and the
+    // sectors' alpha (hb_prf_pair_kernel) + hb_mac_kernel, no prefix image
+    // and no retry pass ($HB_NO_SMALL_ENCODE, test switch: the two-pass
+    // engine for every size).
+    const u64 cb0 = C ? ((256ull << 20) / C ? (256ull << 20) / C : 1) : 1;
+    const u64 launch_max = (flags & HB_DATA_ON_DEVICE) ? nblocks : (nblocks < cb0 ? nblocks : cb0);
+    const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max && use_quad(c, launch_max + S) &&
+                       !sw_env(c, "HB_NO_SMALL_ENCODE");
+    int rc = 0;
+    if (!small) {
+        rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, cxx ? 1 : 0);
+        if (rc) return rc;
+        mark("alpha PRF");
+        rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S);
+        if (rc) return rc;
+        mark("alpha PRF + Montgomery");
+    }
 
     EncodeArgs<NL> A;
     memset(&A, 0, sizeof A);
-    // Small inputs -- as many blocks per launch as the quad engine runs at once
-    // (use_quad): F from one placed quad-engine PRF launch + hb_mac_kernel,
-    // no prefix image and no retry pass ($HB_NO_SMALL_ENCODE, test switch:
-    // the two-pass engine for every size).
-    const u64 cb0 = C ? ((256ull << 20) / C ? (256ull << 20) / C : 1) : 1;
-    const u64 launch_max = (flags & HB_DATA_ON_DEVICE) ? nblocks : (nblocks < cb0 ? nblocks : cb0);
-    const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max && use_quad(c, launch_max) &&
-                       !sw_env(c, "HB_NO_SMALL_ENCODE");
     int mf_layout = 0;   // MFMA MAC table layout (0: VALU MAC)
     if constexpr (NL == 8) {
         // MFMA MAC tables (hb_mfma_block_acc): 256-bit primes with whole
@@ -960,7 +968,8 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     A.ss = pi.ss;
     A.S = S;
     unsigned long long *q0 = c->queue, *q7 = c->queue + HB_QSLOT * HB_SLOT_RETRY;
-    HB_CHECK(hipMemsetAsync(q0, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+    // slots 0 (first pass / small-input F) and 1 (alpha)
+    HB_CHECK(hipMemsetAsync(q0, 0, 2 * HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
     HB_CHECK(hipMemsetAsync(q7, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
 
     const bool tags_dev = flags & HB_TAGS_ON_DEVICE;
@@ -1027,6 +1036,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         mark("MFMA tables");
     }
 
+    bool alpha_todo = small;   // the first small-input launch computes alpha too
     auto launch = [&](const uint8_t *d, u64 dlen, u64 nb, u64 base, uint8_t *tg) -> int {
         A.data = d;
         A.len = dlen;
@@ -1036,19 +1046,44 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         const int align = full16(pi, NL, C, d) ? 16 : 1;
         if (small) {
             // F(base + k): placed quad waves, queue slot 0 not cleared per
-            // chunk (no job counter; tries and abandoned jobs add up)
-            PrfArgs<NL> F;
-            memset(&F, 0, sizeof F);
+            // chunk (no job counter; tries and abandoned jobs add up); the
+            // first launch also computes alpha_j R mod p beside them
+            Prf2Args<NL> F2;
+            memset(&F2, 0, sizeof F2);
+            PrfArgs<NL> &F = F2.f;
             F.prf = A.prf;
             F.x0 = base;
             F.n = nb;
             F.out = (u32 *)c->vals.p;
             F.t0 = c->t0;
             F.queue = q0;
-            const EngineShape es = quad_engine(c, nb);
+            if (alpha_todo) {
+                int nra = 0;
+                if (!make_prf<NL>(a_key, key_len, p_be, p_len, F2.pa, nra) || nra != nr) {
+                    // (a different AES key length for alpha: its own launch first)
+                    rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, 0);
+                    if (rc) return rc;
+                    rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S);
+                    if (rc) return rc;
+                    F2.S = 0;
+                } else {
+                    F2.S = S;
+                }
+                F2.mod = A.mod;
+                const Limbs &r2 = r2_of(c, p, NL);
+                for (int t = 0; t < NL; ++t) F2.r2[t] = r2[t];
+                F2.amont = (u32 *)c->alpha_mont.p;
+                F2.aqueue = q0 + HB_QSLOT;
+                alpha_todo = false;
+            }
+            const EngineShape es = quad_engine(c, nb + F2.S);
             F.qchunk = es.chunk;
             F.place = 1;
-            HB_CHECK(hb_launch_prf<NL>(F, nr, 3, es.grid, c->stream), "hb_prf_kernel launch");
+            if (F2.S) {
+                HB_CHECK(hb_launch_prf_pair<NL>(F2, nr, es.grid, c->stream), "hb_prf_pair_kernel launch");
+            } else {
+                HB_CHECK(hb_launch_prf<NL>(F, nr, 3, es.grid, c->stream), "hb_prf_kernel launch");
+            }
             HB_CHECK(hb_launch_mac<NL>(A, align, c->stream), "hb_mac_kernel launch");
             c->last_launches += 2;
             return 0;
@@ -1097,8 +1132,12 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(c->data[1].ensure((size_t)(cb * C)), "hipMalloc(staging)");
         std::unique_ptr<HostWindows> hw, tw;
         try {   // (a helper thread that cannot be started: copy unpinned)
-            if ((flags & HB_HOST_REGISTER) && len) hw.reset(new HostWindows(c, data, len, true));
-            if ((flags & HB_HOST_REGISTER) && !tags_dev)
+            // (below 32 MiB the windows' helper threads and page-locking cost
+            // more than the pageable copy they would speed up: a 1 MiB file
+            // waited ~150 us for its first window, profiles/r05/w)
+            const bool reg = (flags & HB_HOST_REGISTER) && len >= (32ull << 20);
+            if (reg) hw.reset(new HostWindows(c, data, len, true));
+            if (reg && !tags_dev)
                 tw.reset(new HostWindows(c, tags, nblocks * pi.tw, false, (double)pi.tw / (double)C));
         } catch (const std::exception &) {
             hw.reset();

@@ -67,7 +67,8 @@ extern "C" {
                                  done), instead of the runtime's pageable staging.
                                  For read-only mappings of files (the reference's
                                  file object, PySwizzle.py:299) and other large host
-                                 buffers; a window that cannot be registered (e.g.
+                                 buffers (files under 32 MiB are copied pageable:
+                                 the windows would cost more than they save); a window that cannot be registered (e.g.
                                  already registered by the caller) is copied as is.
                                  Same tags. */
 
