@@ -261,3 +261,61 @@ def test_host_prove_upload_equals_gather_and_oracle(oracle, monkeypatch, bits, S
         monkeypatch.delenv("HB_NO_PROVE_UPLOAD", raising=False)
     if uploaded and bits <= 512:
         assert launches[0] == 1      # the fused launch on the uploaded file
+
+
+def test_concurrent_contexts_fused_proves_and_verifies(oracle):
+    """Two contexts on one GPU (heartbeat_amd.multi's repeated-device
+    instances), each driven by its own host thread, run fused proves and
+    verifies at the same time: each context's counters, limb sums and result
+    buffer are its own, and no fused launch waits on another workgroup, so
+    the interleaving neither deadlocks nor mixes results.  All == the oracle."""
+    import threading
+    from heartbeat_amd import _native as nat
+    L = nat.lib()
+    p = _prime(256)
+    w = nat.width_of(p)
+    S, n, chunks = 16, 4 << 20, 10000
+    data = np.random.default_rng(21).integers(0, 256, n, dtype=np.uint8).tobytes()
+    fk, ak = b"x" * 32, b"y" * 32
+    tags = oracle.encode(p, S, fk, ak, data, nthreads=8)
+    traw = np.frombuffer(b"".join(t.to_bytes(w, "big") for t in tags), dtype=np.uint8)
+    pb = nat.be(p)
+    keys = [hashlib.sha256(b"cc%d" % k).digest() for k in range(6)]
+    want = {k: oracle.prove(p, S, key, chunks, p, tags, data) for k, key in enumerate(keys)}
+    errors, got = [], {}
+
+    def worker(inst, ks):
+        try:
+            ctx = nat.context(0, inst)
+            dd, dt = ctypes.c_void_p(), ctypes.c_void_p()
+            ctx.check(L.hb_device_malloc(ctx.h, n, ctypes.byref(dd)))
+            ctx.check(L.hb_device_malloc(ctx.h, len(traw), ctypes.byref(dt)))
+            try:
+                ctx.check(L.hb_memcpy(ctx.h, dd, np.frombuffer(data, dtype=np.uint8).ctypes.data, n, 1))
+                ctx.check(L.hb_memcpy(ctx.h, dt, traw.ctypes.data, len(traw), 1))
+                for rep in range(5):
+                    for k in ks:
+                        mu = ctypes.create_string_buffer(w * S)
+                        sg = ctypes.create_string_buffer(w)
+                        ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, keys[k], 32, chunks, pb, len(pb), dt, len(tags),
+                                             dd, n, 3, mu, sg))
+                        rhs = ctypes.create_string_buffer(w)
+                        ctx.check(L.hb_verify_rhs(ctx.h, pb, len(pb), S, fk, ak, 32, len(tags), keys[k], 32, chunks,
+                                                  pb, len(pb), mu.raw, rhs))
+                        got[(inst, rep, k)] = (_ints(mu.raw, w, S), int.from_bytes(sg.raw, "big"),
+                                               rhs.raw == sg.raw)
+            finally:
+                ctx.check(L.hb_device_free(ctx.h, dd))
+                ctx.check(L.hb_device_free(ctx.h, dt))
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(i + 1, [0, 1, 2] if i == 0 else [3, 4, 5])) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not errors, errors
+    assert len(got) == 2 * 5 * 3
+    for (inst, rep, k), (mu, sg, ok) in got.items():
+        assert (mu, sg) == want[k] and ok, (inst, rep, k)
