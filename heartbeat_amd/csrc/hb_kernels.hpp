@@ -386,6 +386,19 @@ template <int NL>
 #define HB_OCC8 4
 #endif
 struct HbEncodeOcc { static constexpr int v = NL <= 8 ? HB_OCC8 : 1; };
+// Threads per workgroup of the encode kernels: 1,024 (16 waves sharing one
+// LDS table image per CU), but 512 for primes above 512 bits, whose 2NL+1-limb
+// MAC accumulator, REDC and PRF output do not fit the 128 VGPRs a lane of a
+// 1,024-thread workgroup gets (NL = 32 spilled 576-656 B per lane): 256
+// VGPRs, 8 waves per CU.
+#ifndef HB_WIDE_WG
+#define HB_WIDE_WG 512
+#endif
+#ifndef HB_WIDE_NL
+#define HB_WIDE_NL 32
+#endif
+template <int NL>
+struct HbEncodeWg { static constexpr int v = NL >= HB_WIDE_NL ? HB_WIDE_WG : HB_ENGINE_WG; };
 
 
 __device__ __forceinline__ void hb_zero_sr(u32 sr[4]) { sr[0] = sr[1] = sr[2] = sr[3] = 0; }
@@ -413,7 +426,7 @@ struct EncodeHandler {
 };
 
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_encode_kernel(EncodeArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
@@ -442,7 +455,7 @@ __global__ __launch_bounds__(256) void hb_mac_kernel(EncodeArgs<NL> A) {
 // engine and MAC with the cxx prf (CFB-128: nb/16 full AES per try instead of
 // nb byte-0 AES).
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_cxx_encode_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_cxx_encode_kernel(EncodeArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
@@ -916,7 +929,7 @@ __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const L
 }
 
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
     // MFMA MAC for 256-bit primes with aligned full-width sectors (A.mfma set by the host)
     constexpr bool MF = NL == 8 && ALIGN == 16;
     // MF: the T-table image plus the MFMA A fragments (HB_MFMA_NT x S x 1 KiB,
@@ -1031,7 +1044,7 @@ struct RetryHandler {
 };
 
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HB_ENGINE_WG, HbEncodeOcc<NL>::v) void hb_encode_retry_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_encode_retry_kernel(EncodeArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     // pass 1 has completed (stream order): the count is final
     const u64 cnt = *(volatile unsigned long long *)A.retry_count;
@@ -1943,7 +1956,7 @@ __host__ inline void hb_load_kernel(K *k) {
 // 3 = cxx prf encode
 template <int NL, int PASS>
 hipError_t hb_launch_encode_pass(const EncodeArgs<NL> &A, int nr, int align, int grid, hipStream_t s) {
-    dim3 g(grid), b(HB_ENGINE_WG);
+    dim3 g(grid), b(HbEncodeWg<NL>::v);
 #define HB_ENC(K, NRV, AL) HB_LAUNCH((K<NL, NRV, AL>), g, b, s, A)
 #define HB_ENC_NR(K, AL) \
     do { if (nr == 14) HB_ENC(K, 14, AL); else if (nr == 12) HB_ENC(K, 12, AL); else HB_ENC(K, 10, AL); } while (0)

@@ -756,21 +756,38 @@ HB_HD void hb_mac(u32 acc[2 * NL + 1], const u32 *a, const u32 b[NL]) {
 // Montgomery reduction of acc (2NL+1 limbs, value T): v = (T + M p) / R with
 // v < T/R + p, NL+1 limbs.
 template <int NL>
+HB_HD void hb_redc_row(u32 *acc, const ModP<NL> &P, int i, u32 &extra) {
+    u32 q = acc[i] * P.pinv;
+    u64 carry = 0;
+    HB_UNROLL
+    for (int b = 0; b < NL; ++b) {
+        u64 t = (u64)q * P.p[b] + acc[i + b] + carry;
+        acc[i + b] = (u32)t;
+        carry = t >> 32;
+    }
+    u64 t = (u64)acc[i + NL] + carry + extra;
+    acc[i + NL] = (u32)t;
+    extra = (u32)(t >> 32);
+}
+
+// Rows I.. of the reduction with compile-time row indices: at NL = 32 the
+// compiler leaves a plain outer loop rolled (32 x 32 MACs is past its unroll
+// budget), which indexes acc dynamically and moves it to scratch.
+template <int NL, int I>
+HB_HD void hb_redc_rows(u32 *acc, const ModP<NL> &P, u32 &extra) {
+    if constexpr (I < NL) {
+        hb_redc_row<NL>(acc, P, I, extra);
+        hb_redc_rows<NL, I + 1>(acc, P, extra);
+    }
+}
+
+template <int NL>
 HB_HD void hb_redc(u32 acc[2 * NL + 1], const ModP<NL> &P, u32 v[NL + 1]) {
     u32 extra = 0;
-    HB_UNROLL
-    for (int i = 0; i < NL; ++i) {
-        u32 q = acc[i] * P.pinv;
-        u64 carry = 0;
-        HB_UNROLL
-        for (int b = 0; b < NL; ++b) {
-            u64 t = (u64)q * P.p[b] + acc[i + b] + carry;
-            acc[i + b] = (u32)t;
-            carry = t >> 32;
-        }
-        u64 t = (u64)acc[i + NL] + carry + extra;
-        acc[i + NL] = (u32)t;
-        extra = (u32)(t >> 32);
+    if constexpr (NL <= 32) {
+        hb_redc_rows<NL, 0>(acc, P, extra);
+    } else {   // NL = 64 does not fit the register file either way
+        for (int i = 0; i < NL; ++i) hb_redc_row<NL>(acc, P, i, extra);
     }
     acc[2 * NL] += extra;
     HB_UNROLL
