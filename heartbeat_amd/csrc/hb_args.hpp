@@ -217,6 +217,15 @@ struct VerifyArgs {
 // (cmax x tw); returns the arena's size.
 #define HB_FZ_BYTES 30720
 #define HB_FZ_MAXJOBS 48
+// Widest prime (limbs) the fused prove and verify take.  At 32 limbs their
+// summer and alpha waves spill (a 2NL+1-limb accumulator under a 1,024-thread
+// workgroup's 128 VGPRs: 760 B of scratch per lane), but off the PRF chains
+// that bound the launch: PySwizzle's defaults (1024-bit, 820 chunks) verify
+// in 0.46-0.79 vs 0.86-1.71 ms as a launch sequence, prove 2-5 % faster
+// (same box, three seeded primes and key sets; profiles/r05/f32).
+#ifndef HB_FUSE_MAX_NL
+#define HB_FUSE_MAX_NL 32
+#endif
 HB_HHD u64 hb_fz_layout(u32 cmax, u32 nl, u32 ncols, u64 C, u32 tw, u32 off[5]) {
     u64 o = (2ull * cmax + 4) * 4;
     off[0] = 0;

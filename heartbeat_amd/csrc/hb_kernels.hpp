@@ -2060,7 +2060,7 @@ hipError_t hb_launch_prove_prf(const ProveArgs<NL> &A, int nr, int mode_i, int m
     return hipGetLastError();
 }
 
-// fused verify (NL <= 16; every key with nr AES rounds)
+// fused verify (NL <= HB_FUSE_MAX_NL; every key with nr AES rounds)
 template <int NL>
 hipError_t hb_launch_verify_fused(const VerifyArgs<NL> &A, int nr, int grid, hipStream_t s) {
     dim3 g(grid), b(HB_ENGINE_WG);

@@ -392,7 +392,7 @@ void prepare_nl(hb_ctx *c) {
     PrfArgs<NL> P;
     memset(&P, 0, sizeof P);
     for (int mode : {0, 3}) (void)hb_launch_prf<NL>(P, 14, mode, 0, c->stream);
-    if constexpr (NL <= 16) {
+    if constexpr (NL <= HB_FUSE_MAX_NL) {
         VerifyArgs<NL> VA;
         memset(&VA, 0, sizeof VA);
         (void)hb_launch_verify_fused<NL>(VA, 14, 0, c->stream);
@@ -1224,6 +1224,18 @@ int ensure_ctl(hb_ctx *c, u32 ncols) {
     return 0;
 }
 
+// The fused launches' limb sums: zero between operations (each closer
+// re-zeroes what it used), so a grown buffer is zeroed whole.  Growth is
+// told by the size, not the address: hipFree + hipMalloc may hand back the
+// same address, and a pointer comparison then left the new tail holding stale
+// memory (a wrong sigma after a prove with fewer columns on the context).
+int ensure_facc(hb_ctx *c, size_t bytes) {
+    const size_t had = c->facc.n;
+    HB_CHECK(c->facc.ensure(bytes), "hipMalloc(facc)");
+    if (c->facc.n != had) HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync(facc)");
+    return 0;
+}
+
 unsigned int *flags_word(hb_ctx *c) { return (unsigned int *)c->ctl.p + (c->ctl.n / sizeof(unsigned int) - 1); }
 
 int ensure_hres(hb_ctx *c, size_t words) {
@@ -1522,17 +1534,15 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     PA.place = quad && pwaves <= 16ull * (u64)pgrid && !sw_env(c, "HB_NO_PROVE_PLACE") ? 1u : 0u;
     // Fused weighted sums (hb_prove_fused): placed quad waves, a device
     // gather, at most 48 jobs per workgroup whose blocks, tags and sums fit
-    // the LDS arena, primes up to 512 bits (the summers' registers);
+    // the LDS arena, primes up to HB_FUSE_MAX_NL limbs (the summers' registers);
     // $HB_NO_PROVE_FUSE (test switch, A/B): the PRF launch + hb_wsum_kernel
     const u64 fcmax = (n + (u64)pgrid - 1) / (u64)pgrid;
     u32 fzoff[5];
-    const bool fuse = dev_gather && PA.place && NL <= 16 && ncols <= 256 && fcmax <= HB_FZ_MAXJOBS &&
+    const bool fuse = dev_gather && PA.place && NL <= HB_FUSE_MAX_NL && ncols <= 256 && fcmax <= HB_FZ_MAXJOBS &&
                       hb_fz_layout((u32)fcmax, NL, ncols, C, pi.tw, fzoff) <= HB_FZ_BYTES &&
                       !sw_env(c, "HB_NO_PROVE_FUSE");
     if (fuse) {
-        const void *was = c->facc.p;
-        HB_CHECK(c->facc.ensure((size_t)ncols * NL * 8), "hipMalloc(facc)");
-        if (c->facc.p != was) HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync(facc)");
+        if (int rc = ensure_facc(c, (size_t)ncols * NL * 8)) return rc;
         if (c->ctl_dirty) {
             HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync(ctl)");
             HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync(facc)");
@@ -1706,7 +1716,7 @@ int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     const bool check_all = cxx && chunks >= state_chunks;
     if (check_all) chunks = state_chunks;
     c->last_launches = 0;
-    if constexpr (NL <= 16) {
+    if constexpr (NL <= HB_FUSE_MAX_NL) {
         // One launch (hb_verify_fused_kernel) when the quad engine takes the
         // challenge, every workgroup's share fits its LDS arena, alpha fits 16
         // jobs per workgroup and all four keys have the same AES round count;
@@ -1736,9 +1746,7 @@ int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
                     c->ctl_dirty = false;
                 }
                 if (int rc = ensure_ctl(c, 1)) return rc;
-                const void *was = c->facc.p;
-                HB_CHECK(c->facc.ensure((size_t)NL * 8), "hipMalloc(facc)");
-                if (c->facc.p != was) HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync");
+                if (int rc = ensure_facc(c, (size_t)NL * 8)) return rc;
                 if (c->ctl_dirty) {
                     HB_CHECK(hipMemsetAsync(c->ctl.p, 0, c->ctl.n, c->stream), "hipMemsetAsync(ctl)");
                     HB_CHECK(hipMemsetAsync(c->facc.p, 0, c->facc.n, c->stream), "hipMemsetAsync(facc)");

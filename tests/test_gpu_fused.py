@@ -5,7 +5,7 @@ halves arrive; the last workgroup finishes the sums.  Every case is proved
 three times on one context -- fused, with HB_NO_PROVE_FUSE (PRF launch +
 hb_wsum_kernel), and fused again -- and each must equal the oracle.  The launch count tells
 which path ran (1 = fused): the cases cover the shapes the host admits (48
-jobs per workgroup and one more, NL = 8 and 16, 16-byte and byte-wise sector
+jobs per workgroup and one more, NL = 8, 16 and 32, 16-byte and byte-wise sector
 and tag loads, 2 to 65 columns, empty and ragged files, repeated proves on
 one context: the limb sums and counters re-zeroed by each launch's closer).
 
@@ -49,6 +49,9 @@ CASES = [
     (512, 3, 300000, 4000, True),                # NL = 16, 16-byte sector loads
     (384, 7, 250000, 2500, True),                # NL = 16, 48-byte sectors: byte-wise loads
     (128, 16, 100000, 1000, True),               # NL = 8, 16-byte sectors and tags: byte-wise loads
+    (1024, 10, 1 << 20, 820, True),              # NL = 32, PySwizzle's defaults and default challenge
+    (1020, 16, 200000, 2000, True),              # NL = 32, 127-byte sectors: byte-wise loads
+    (1000, 2, 150000, 3000, False),              # NL = 32, 125-byte sectors and tags: host-layout gather
 ]
 
 
@@ -170,7 +173,9 @@ VERIFY_CASES = [
     (256, 100, 4000, 1000, 32, True),            # alpha over several workgroups (100 > 16)
     (512, 3, 9000, 4000, 16, True),              # NL = 16, AES-128 keys (NR = 10)
     (384, 7, 77777, 2500, 24, True),             # NL = 16, AES-192 keys (NR = 12)
-    (1024, 4, 5000, 1000, 32, False),            # NL = 32: the launch sequence
+    (1024, 4, 5000, 1000, 32, True),             # NL = 32
+    (1024, 10, 820, 820, 32, True),              # NL = 32, PySwizzle's defaults (1 MiB file)
+    (2048, 4, 5000, 1000, 32, False),            # NL = 64: the launch sequence
 ]
 
 
@@ -219,7 +224,7 @@ def test_fused_verify_equals_launch_sequence_and_oracle(oracle, monkeypatch, bit
 
 @pytest.mark.parametrize("bits,S,nbytes,chunks,uploaded", [
     (256, 16, 1 << 20, 2049, True),             # a 1 MiB file and its default challenge: uploaded, fused
-    (1024, 10, 1 << 20, 820, True),             # PySwizzle's defaults: uploaded, two launches (NL = 32)
+    (1024, 10, 1 << 20, 820, True),             # PySwizzle's defaults: uploaded, fused (NL = 32)
     (256, 1, (5 << 20) + 3, 3000, True),        # under 8 MiB: uploaded
     (256, 16, 16 << 20, 10000, False),          # 16 MiB > 2 x 5.1 MB of challenged blocks: host gather
 ])
@@ -259,7 +264,7 @@ def test_host_prove_upload_equals_gather_and_oracle(oracle, monkeypatch, bits, S
             assert (_ints(mu.raw, w, S), int.from_bytes(sg.raw, "big")) == want, (bits, S, nbytes, off)
     finally:
         monkeypatch.delenv("HB_NO_PROVE_UPLOAD", raising=False)
-    if uploaded and bits <= 512:
+    if uploaded:
         assert launches[0] == 1      # the fused launch on the uploaded file
 
 
