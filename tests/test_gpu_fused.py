@@ -324,3 +324,51 @@ def test_concurrent_contexts_fused_proves_and_verifies(oracle):
     assert len(got) == 2 * 5 * 3
     for (inst, rep, k), (mu, sg, ok) in got.items():
         assert (mu, sg) == want[k] and ok, (inst, rep, k)
+
+
+def test_fused_sums_after_limb_buffer_growth(oracle):
+    """On a fresh context, fused proves whose column counts (and limb widths)
+    keep growing the limb-sum buffer, each followed by a fused verify: the
+    grown buffer must start at zero wherever the allocator places it (a
+    reallocation at the same address once left a stale tail there and a wrong
+    sigma).  Each proof == the oracle, each verify accepts it."""
+    from heartbeat_amd import _native as nat
+    ctx = nat.context(0, 3)
+    L = nat.lib()
+    rng = np.random.default_rng(77)
+    n = 1 << 19
+    data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    dd = ctypes.c_void_p()
+    ctx.check(L.hb_device_malloc(ctx.h, n, ctypes.byref(dd)))
+    try:
+        ctx.check(L.hb_memcpy(ctx.h, dd, np.frombuffer(data, dtype=np.uint8).ctypes.data, n, 1))
+        for k, (bits, S) in enumerate([(256, 1), (256, 2), (256, 5), (1024, 4), (256, 16), (1024, 10), (256, 40),
+                                       (256, 64)]):
+            p = _prime(bits)
+            w = nat.width_of(p)
+            fk, ak = hashlib.sha256(b"gr-f%d" % k).digest(), hashlib.sha256(b"gr-a%d" % k).digest()
+            tags = oracle.encode(p, S, fk, ak, data, nthreads=8)
+            traw = np.frombuffer(b"".join(t.to_bytes(w, "big") for t in tags), dtype=np.uint8)
+            dt = ctypes.c_void_p()
+            ctx.check(L.hb_device_malloc(ctx.h, len(traw), ctypes.byref(dt)))
+            try:
+                ctx.check(L.hb_memcpy(ctx.h, dt, traw.ctypes.data, len(traw), 1))
+                pb, key = nat.be(p), hashlib.sha256(b"gr-c%d" % k).digest()
+                chunks = min(len(tags), 2000)
+                mu = ctypes.create_string_buffer(w * S)
+                sg = ctypes.create_string_buffer(w)
+                ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, key, 32, chunks, pb, len(pb), dt, len(tags), dd, n, 3,
+                                     mu, sg))
+                ms, nl = ctypes.c_double(), ctypes.c_uint32()
+                ctx.check(L.hb_last_kernel_ms(ctx.h, ctypes.byref(ms), ctypes.byref(nl)))
+                assert nl.value == 1, (bits, S, nl.value)
+                assert (_ints(mu.raw, w, S), int.from_bytes(sg.raw, "big")) == \
+                    oracle.prove(p, S, key, chunks, p, tags, data), (bits, S)
+                rhs = ctypes.create_string_buffer(w)
+                ctx.check(L.hb_verify_rhs(ctx.h, pb, len(pb), S, fk, ak, 32, len(tags), key, 32, chunks, pb, len(pb),
+                                          mu.raw, rhs))
+                assert rhs.raw == sg.raw, (bits, S)
+            finally:
+                ctx.check(L.hb_device_free(ctx.h, dt))
+    finally:
+        ctx.check(L.hb_device_free(ctx.h, dd))
