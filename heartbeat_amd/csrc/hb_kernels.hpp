@@ -451,6 +451,56 @@ __global__ __launch_bounds__(256) void hb_mac_kernel(EncodeArgs<NL> A) {
     hb_store_tag<NL, ALIGN>(A.tags + k * (u64)A.tw, A.tw, tag);
 }
 
+// hb_mac_kernel with the sectors of a block spread over S lanes (S <= T): lane
+// (k, j) forms alpha_j R * m_kj (+ F_k R on lane j = 0) and reduces it
+// (REDC: alpha_j m_kj [+ F_k] mod p), and lane (k, 0) adds the S residues mod
+// p.  A small input has too few blocks to fill the GPU with one lane each
+// (820 at PySwizzle's defaults on 1 MiB: four workgroups, every lane a serial
+// chain of S x NL^2 multiply-adds); this cuts the chain to NL^2 + REDC.
+// Sector values as hb_block_tag's: BE(data[off, min(off + ss, len))), 0 past
+// the end of the file.
+template <int NL>
+struct HbMacSplit { static constexpr int T = NL >= 64 ? 128 : 256; };
+template <int NL, int ALIGN>
+__global__ __launch_bounds__(HbMacSplit<NL>::T) void hb_mac_split_kernel(EncodeArgs<NL> A) {
+    constexpr int T = HbMacSplit<NL>::T;
+    __shared__ u32 red[T * NL];
+    const u32 S = A.S, bpw = T / S;
+    const u32 lb = threadIdx.x / S, j = threadIdx.x % S;
+    const u64 k = (u64)blockIdx.x * bpw + lb;
+    const bool live = lb < bpw && k < A.nblocks;
+    if (live) {
+        u32 acc[2 * NL + 1], m[NL];
+        for (int t = 0; t <= 2 * NL; ++t) acc[t] = 0;
+        if (j == 0)
+            for (int t = 0; t < NL; ++t) acc[NL + t] = A.fv[k * NL + t];
+        const u64 off = k * A.C + (u64)j * A.ss;
+        if (off < A.len) {
+            const u32 r = (u32)(A.len - off < A.ss ? A.len - off : A.ss);
+            if (ALIGN == 16 && r == A.ss) hb_load_full16<NL>(A.data, off, m);
+            else hb_load_be_bytes<NL>(A.data, off, r, m);
+            hb_mac<NL>(acc, A.alpha_mont + (u64)j * NL, m);
+        }
+        u32 v[NL + 1], res[NL];
+        hb_redc<NL>(acc, A.mod, v);
+        hb_reduce_small<NL>(v, A.mod, res);
+        for (int t = 0; t < NL; ++t) red[threadIdx.x * NL + t] = res[t];
+    }
+    __syncthreads();
+    if (!live || j != 0) return;
+    u32 v[NL + 1], tag[NL];
+    u64 c = 0;
+    for (int t = 0; t < NL; ++t) {   // S residues < p: the sum < S p < 2^32 p
+        c += red[threadIdx.x * NL + t];
+        for (u32 i = 1; i < S; ++i) c += red[(threadIdx.x + i) * NL + t];
+        v[t] = (u32)c;
+        c >>= 32;
+    }
+    v[NL] = (u32)c;
+    hb_reduce_small<NL>(v, A.mod, tag);
+    hb_store_tag<NL, ALIGN>(A.tags + k * (u64)A.tw, A.tw, tag);
+}
+
 // The cxx Swizzle encode (shacham_waters_private.cxx:638-702): the same
 // engine and MAC with the cxx prf (CFB-128: nb/16 full AES per try instead of
 // nb byte-0 AES).
@@ -1982,6 +2032,18 @@ hipError_t hb_launch_prf_pair(const Prf2Args<NL> &A, int nr, int grid, hipStream
 
 template <int NL>
 hipError_t hb_launch_mac(const EncodeArgs<NL> &A, int align, hipStream_t s) {
+    constexpr u32 T = HbMacSplit<NL>::T;
+    if (A.S >= 2 && A.S <= T && !hb_load_only) {
+        const u32 bpw = T / A.S;
+        const u64 g = (A.nblocks + bpw - 1) / bpw;
+        if (align == 16) HB_LAUNCH((hb_mac_split_kernel<NL, 16>), dim3((u32)g), dim3(bpw * A.S), s, A);
+        else HB_LAUNCH((hb_mac_split_kernel<NL, 1>), dim3((u32)g), dim3(bpw * A.S), s, A);
+        return hipGetLastError();
+    }
+    if (hb_load_only) {
+        hb_load_kernel(&hb_mac_split_kernel<NL, 16>);
+        hb_load_kernel(&hb_mac_split_kernel<NL, 1>);
+    }
     const u64 grid = (A.nblocks + 255) / 256;
     if (align == 16) HB_LAUNCH((hb_mac_kernel<NL, 16>), dim3((u32)grid), dim3(256), s, A);
     else HB_LAUNCH((hb_mac_kernel<NL, 1>), dim3((u32)grid), dim3(256), s, A);

@@ -699,9 +699,15 @@ def test_prove_mixed_residency_equals_device(nat, oracle):
     (256, 16, 65536 * 512),                 # one block more: the two-pass engine
     (256, 1, (3 << 20) + 7),                # S = 1, ragged tail
     (384, 3, 200000),                       # 48-byte sectors: byte-wise MAC loads
+    (1024, 10, (1 << 20) + 333),            # NL = 32, ragged tail: a short sector, then none
+    (1020, 16, 300001),                     # NL = 32, 127-byte sectors
+    (2048, 4, 100000),                      # NL = 64: 128-lane workgroups of the split MAC
+    (512, 200, 1 << 20),                    # one block per 200-lane workgroup
+    (256, 300, 1 << 20),                    # S > 256: one lane per block (hb_mac_kernel)
 ])
 def test_small_encode_equals_two_pass_and_oracle(nat, oracle, monkeypatch, bits, S, nbytes):
-    """Small inputs take the quad-PRF + hb_mac_kernel path; the same encode
+    """Small inputs take the quad-PRF + MAC-kernel path (the sectors of a
+    block over S lanes, hb_mac_split_kernel, for 2 <= S <= 256); the same encode
     forced through the two-pass engine (HB_NO_SMALL_ENCODE) and the oracle
     agree, from device memory and from host memory through the drop-in API.
     Reference: PySwizzle.py:279-314."""
