@@ -198,6 +198,7 @@ const SwitchName kSwitches[] = {
     {"HB_NO_VERIFY_FUSE", HB_SW_NO_VERIFY_FUSE},
     {"HB_NO_SMALL_ENCODE", HB_SW_NO_SMALL_ENCODE},
     {"HB_NO_PROVE_UPLOAD", HB_SW_NO_PROVE_UPLOAD},
+    {"HB_MID_BLOCKS", HB_SW_MID_BLOCKS},
 };
 
 int nl_for_bits(int bits) {
@@ -909,8 +910,15 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // engine for every size).
     const u64 cb0 = C ? ((256ull << 20) / C ? (256ull << 20) / C : 1) : 1;
     const u64 launch_max = (flags & HB_DATA_ON_DEVICE) ? nblocks : (nblocks < cb0 ? nblocks : cb0);
-    const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max && use_quad(c, launch_max + S) &&
-                       !sw_env(c, "HB_NO_SMALL_ENCODE");
+    // Mid-size inputs (up to $HB_MID_BLOCKS blocks per launch, A/B switch):
+    // the same two launches with the quad engine on a job queue instead of
+    // placed waves -- quads refill as their jobs finish, and a launch's
+    // longest rejection chain runs at the quad engine's round latency
+    // instead of a lone lane's.
+    const char *mid_env = sw_env(c, "HB_MID_BLOCKS");
+    const u64 mid_max = mid_env ? strtoull(mid_env, nullptr, 10) : 0;
+    const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max &&
+                       (use_quad(c, launch_max + S) || launch_max <= mid_max) && !sw_env(c, "HB_NO_SMALL_ENCODE");
     int rc = 0;
     if (!small) {
         rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, cxx ? 1 : 0);
@@ -1057,9 +1065,10 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             F.out = (u32 *)c->vals.p;
             F.t0 = c->t0;
             F.queue = q0;
+            const bool placed = use_quad(c, nb + S);
             if (alpha_todo) {
                 int nra = 0;
-                if (!make_prf<NL>(a_key, key_len, p_be, p_len, F2.pa, nra) || nra != nr) {
+                if (!placed || !make_prf<NL>(a_key, key_len, p_be, p_len, F2.pa, nra) || nra != nr) {
                     // (a different AES key length for alpha: its own launch first)
                     rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, 0);
                     if (rc) return rc;
@@ -1078,8 +1087,11 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             }
             const EngineShape es = quad_engine(c, nb + F2.S);
             F.qchunk = es.chunk;
-            F.place = 1;
-            if (F2.S) {
+            F.place = placed ? 1u : 0u;
+            if (!placed) {   // queue: one job per quad per refill, every CU
+                HB_CHECK(hipMemsetAsync(q0, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
+                HB_CHECK(hb_launch_prf<NL>(F, nr, 3, (int)c->num_cus, c->stream), "hb_prf_kernel launch");
+            } else if (F2.S) {
                 HB_CHECK(hb_launch_prf_pair<NL>(F2, nr, es.grid, c->stream), "hb_prf_pair_kernel launch");
             } else {
                 HB_CHECK(hb_launch_prf<NL>(F, nr, 3, es.grid, c->stream), "hb_prf_kernel launch");
