@@ -910,13 +910,19 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // engine for every size).
     const u64 cb0 = C ? ((256ull << 20) / C ? (256ull << 20) / C : 1) : 1;
     const u64 launch_max = (flags & HB_DATA_ON_DEVICE) ? nblocks : (nblocks < cb0 ? nblocks : cb0);
-    // Mid-size inputs (up to $HB_MID_BLOCKS blocks per launch, A/B switch):
-    // the same two launches with the quad engine on a job queue instead of
-    // placed waves -- quads refill as their jobs finish, and a launch's
-    // longest rejection chain runs at the quad engine's round latency
-    // instead of a lone lane's.
+    // Mid-size inputs (up to 17 x 256 x #CUs blocks per launch: 1,114,112 on
+    // MI355X, so that 2^20 + 1 blocks qualify): the same two launches with
+    // the quad engine on a job queue instead of placed waves -- quads refill
+    // as their jobs finish, the launch's longest rejection chain runs at the
+    // quad engine's round latency instead of a lone lane's, and there is no
+    // prefix image or retry list.  Benchmark prime P256, S = 16: 64 MiB 0.42
+    // vs 1.18 ms, 256 MiB 0.88 vs 1.48, 512 MiB (2^20 + 1 blocks) 1.50 vs
+    // 1.63; S = 1, 2^20 + 1 blocks 1.07 vs 1.58; 1024-bit S = 10, 839 K
+    // blocks 6.54 vs 8.75; but a 256-bit prime with E[tries] 1.95 at 2 M
+    // blocks 3.58 vs 3.32 (profiles/r05/mid).  $HB_MID_BLOCKS (test switch,
+    // A/B): another bound, 0 = none.
     const char *mid_env = sw_env(c, "HB_MID_BLOCKS");
-    const u64 mid_max = mid_env ? strtoull(mid_env, nullptr, 10) : 0;
+    const u64 mid_max = mid_env ? strtoull(mid_env, nullptr, 10) : 17ull * 256ull * (u64)c->num_cus;
     const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max &&
                        (use_quad(c, launch_max + S) || launch_max <= mid_max) && !sw_env(c, "HB_NO_SMALL_ENCODE");
     int rc = 0;

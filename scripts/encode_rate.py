@@ -17,6 +17,8 @@ from oracle import oracle as O            # noqa: E402
 
 
 def prime(bits):
+    if bits == 0:   # "P256": the benchmark's prime (tests/golden/primes.json, E[tries] 1.17)
+        return int(json.load(open("tests/golden/primes.json"))["p256"], 16)
     pys = __import__("heartbeat_amd.PySwizzle.PySwizzle", fromlist=["_is_probable_prime"])
     rng = random.Random(5000 + bits)
     while True:
@@ -26,7 +28,7 @@ def prime(bits):
 
 
 out = []
-for bits, S, gib in [(int(a), int(b), float(c)) for a, b, c in (x.split(":") for x in sys.argv[1:])]:
+for bits, S, gib in [(0 if a == "P256" else int(a), int(b), float(c)) for a, b, c in (x.split(":") for x in sys.argv[1:])]:
     p = prime(bits)
     w = nat.width_of(p)
     C = (p.bit_length() // 8) * S
@@ -40,7 +42,7 @@ for bits, S, gib in [(int(a), int(b), float(c)) for a, b, c in (x.split(":") for
     ctx.check(L.hb_fill_random(ctx.h, d, n, 99))
     fk, ak = hashlib.sha256(b"er-f").digest(), hashlib.sha256(b"er-a").digest()
     pb = nat.be(p)
-    ctx.prepare(bits)
+    ctx.prepare(p.bit_length())
     best = None
     for rep in range(4):
         t0 = time.perf_counter()
@@ -49,7 +51,7 @@ for bits, S, gib in [(int(a), int(b), float(c)) for a, b, c in (x.split(":") for
         kms = ctx.last_kernel_ms()[0]
         if rep and (best is None or dt < best[0]):
             best = (dt, kms)
-    rng = np.random.default_rng(bits)
+    rng = np.random.default_rng(p.bit_length())
     ok = True
     for b in sorted(set(rng.integers(0, nb, 200).tolist()) | {nb - 1}):
         m = min(C, max(0, n - b * C))
@@ -62,6 +64,6 @@ for bits, S, gib in [(int(a), int(b), float(c)) for a, b, c in (x.split(":") for
         ok = ok and int.from_bytes(tg.tobytes(), "big") == want
     ctx.check(L.hb_device_free(ctx.h, d))
     ctx.check(L.hb_device_free(ctx.h, t))
-    out.append({"prime_bits": bits, "sectors": S, "gib": gib, "blocks": nb, "gib_s": round(n / (1 << 30) / best[0], 2),
+    out.append({"prime_bits": bits or "P256", "sectors": S, "gib": gib, "blocks": nb, "gib_s": round(n / (1 << 30) / best[0], 2),
                 "wall_ms": round(best[0] * 1e3, 3), "kernel_ms": round(best[1], 3), "sample_equal_oracle": ok})
     print(json.dumps(out[-1]), flush=True)

@@ -696,7 +696,9 @@ def test_prove_mixed_residency_equals_device(nat, oracle):
 @pytest.mark.parametrize("bits,S,nbytes", [
     (1024, 10, 1 << 20),                    # PySwizzle's defaults on a 1 MiB file
     (256, 16, 65535 * 512),                 # 65,536 blocks: the largest small input (256 CUs)
-    (256, 16, 65536 * 512),                 # one block more: the two-pass engine
+    (256, 16, 65536 * 512),                 # one block more: the quad engine on a job queue
+    (256, 1, 32 << 20),                     # 2^20 + 1 blocks: still the queue (17 x 256 x #CUs)
+    (256, 1, 36 << 20),                     # 1,179,649 blocks: the two-pass engine
     (256, 1, (3 << 20) + 7),                # S = 1, ragged tail
     (384, 3, 200000),                       # 48-byte sectors: byte-wise MAC loads
     (1024, 10, (1 << 20) + 333),            # NL = 32, ragged tail: a short sector, then none
@@ -706,7 +708,9 @@ def test_prove_mixed_residency_equals_device(nat, oracle):
     (256, 300, 1 << 20),                    # S > 256: one lane per block (hb_mac_kernel)
 ])
 def test_small_encode_equals_two_pass_and_oracle(nat, oracle, monkeypatch, bits, S, nbytes):
-    """Small inputs take the quad-PRF + MAC-kernel path (the sectors of a
+    """Small and mid-size inputs (placed quad waves up to 256 x #CUs blocks,
+    then the quad engine on a job queue up to 17 x 256 x #CUs) take the
+    quad-PRF + MAC-kernel path (the sectors of a
     block over S lanes, hb_mac_split_kernel, for 2 <= S <= 256); the same encode
     forced through the two-pass engine (HB_NO_SMALL_ENCODE) and the oracle
     agree, from device memory and from host memory through the drop-in API.
