@@ -376,6 +376,103 @@ __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const Prf
     if (hb_lane_id() == 0 && failed) atomicAdd(queue + 2, (unsigned long long)failed);
 }
 
+// The retry pass's engine (hb_encode_retry_kernel, 256-bit primes): hb_engine
+// (MODE 0) while the job queue lasts; once it is drained and at most 16 lanes
+// of the wave are still inside a rejection chain, each of those chains moves
+// to a quad -- the r-th such lane's job, tries, digest and CFB-8 register
+// (word q to lane q of quad r, the quad engine's layout) -- and finishes on
+// the quad engine's round (hb_quad_prf_try: ~147 clocks per AES round against
+// ~300 for a lone lane running all 16 lookups).  The pass ends on its longest
+// chains, so this halves its tail.  The quads' accept runs the block's
+// finish on one lane (the MFMA path's partial sum + F: cheap at NL = 8).
+#ifndef HB_RETRY_QUAD_TAIL
+#define HB_RETRY_QUAD_TAIL 1
+#endif
+template <int NL, int NR, class H>
+__device__ __forceinline__ void hb_engine_tail(H &h, const LaneTab &L, const PrfParams<NL> &P, u64 njobs,
+                                               unsigned long long *queue) {
+    HbPool pool{0, 0, njobs, queue, false, HB_QUEUE_CHUNK};
+    u64 job = 0;
+    bool active = pool.take(__ballot(1), true, job);
+    u32 dig[8], sr[4] = {0, 0, 0, 0}, out[NL];
+    if (active) {
+        h.init(job, sr);
+        hb_job_digest<0>(h, job, dig, 0);
+    }
+    const u32 resumed = hb_resumed_tries(h, 0);
+    u32 tries = 0, job_tries = resumed, failed = 0;
+    u64 am;
+    while ((am = __ballot(active)) != 0) {
+        if (pool.exhausted && pool.next >= pool.end && __popcll(am) <= 16) break;   // -> quads
+        const u32 ok = hb_prf_try<NL, NR>(L, P, sr, dig, out);
+        tries += active ? 1u : 0u;
+        job_tries += 1u;
+        const bool acc = active && ok;
+        if (acc) h.accept(job, out);
+        const bool give_up = active && !ok && job_tries >= HB_MAX_TRIES;
+        failed += give_up ? 1u : 0u;
+        const bool next = acc || give_up;
+        const u64 m = __ballot(next);
+        if (m) {
+            u64 nj = 0;
+            const bool got = pool.take(m, next, nj);
+            if (next) {
+                active = got;
+                job = nj;
+                job_tries = resumed;
+                if (got) {
+                    h.init(job, sr);
+                    hb_job_digest<0>(h, job, dig, 0);
+                }
+            }
+        }
+    }
+    if (am) {
+        // quad r (lanes 4r .. 4r+3) takes the r-th lane of am
+        const u32 lane = hb_lane_id(), r = lane >> 2, q = lane & 3u;
+        const bool qa = r < (u32)__popcll(am);
+        u64 mm = am;
+        for (u32 k = 0; k < r && mm; ++k) mm &= mm - 1;
+        const int src = mm ? __builtin_ctzll(mm) : 0;
+        const u64 qjob = ((u64)(u32)__shfl((int)(u32)(job >> 32), src) << 32) | (u32)__shfl((int)(u32)job, src);
+        u32 qdig[8];
+        HB_UNROLL
+        for (int t = 0; t < 8; ++t) qdig[t] = (u32)__shfl((int)dig[t], src);
+        const u32 w0 = (u32)__shfl((int)sr[0], src), w1 = (u32)__shfl((int)sr[1], src);
+        const u32 w2 = (u32)__shfl((int)sr[2], src), w3 = (u32)__shfl((int)sr[3], src);
+        u32 s = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+        u32 jt = (u32)__shfl((int)job_tries, src);
+        const QuadLane Q = hb_quad_lane(L);
+        u32 rkq[NR + 1];
+        HB_UNROLL
+        for (int rr = 0; rr <= NR; ++rr) {
+            const u32 k0 = __builtin_amdgcn_readfirstlane(P.rk[4 * rr]), k1 = __builtin_amdgcn_readfirstlane(P.rk[4 * rr + 1]);
+            const u32 k2 = __builtin_amdgcn_readfirstlane(P.rk[4 * rr + 2]), k3 = __builtin_amdgcn_readfirstlane(P.rk[4 * rr + 3]);
+            rkq[rr] = q == 0 ? k0 : q == 1 ? k1 : q == 2 ? k2 : k3;
+        }
+        const bool lead = q == 0;
+        bool qact = qa;
+        u32 qtries = 0, qfailed = 0;
+        while (__ballot(qact)) {
+            const u32 ok = hb_quad_prf_try<NL, NR>(Q, rkq, P, s, qdig, out);
+            qtries += qact && lead ? 1u : 0u;
+            jt += 1u;
+            if (qact && ok && lead) h.accept(qjob, out);
+            const bool give_up = qact && !ok && jt >= HB_MAX_TRIES;
+            qfailed += give_up && lead ? 1u : 0u;
+            if (ok || give_up) qact = false;
+        }
+        tries += qtries;
+        failed += qfailed;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        tries += __shfl_xor(tries, off);
+        failed += __shfl_xor(failed, off);
+    }
+    if (hb_lane_id() == 0 && tries) atomicAdd(queue + 1, (unsigned long long)tries);
+    if (hb_lane_id() == 0 && failed) atomicAdd(queue + 2, (unsigned long long)failed);
+}
+
 // ------------------------------------------------------------------ encode
 // Minimum waves per SIMD requested from the register allocator: 4 (= one
 // 1024-thread workgroup, 16 waves per CU, sharing one 128 KiB LDS table
@@ -1103,7 +1200,8 @@ __global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_enco
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     RetryHandler<NL, ALIGN> h{A};
-    hb_engine<NL, NR>(h, L, A.prf, n, A.queue);
+    if constexpr (NL == 8 && HB_RETRY_QUAD_TAIL) hb_engine_tail<NL, NR>(h, L, A.prf, n, A.queue);
+    else hb_engine<NL, NR>(h, L, A.prf, n, A.queue);
 }
 
 // ------------------------------------------------------------------ PRF batch
