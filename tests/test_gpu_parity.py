@@ -753,3 +753,54 @@ def test_small_encode_equals_two_pass_and_oracle(nat, oracle, monkeypatch, bits,
     want = oracle.encode(p, S, fk, ak, data, nthreads=8) if nb <= 70000 else None
     if want is not None:
         assert split_tags(res[0], w) == want
+
+
+@pytest.mark.parametrize("S,nblocks,check", [
+    (1, 60000, "oracle"),         # every block against the oracle
+    (1, 2 * 1024 * 1024, "mid"),  # 2 M blocks: the two-pass engine against the queued quad engine
+])
+def test_retry_quad_tail_high_rejection(nat, oracle, monkeypatch, S, nblocks, check):
+    """A 256-bit prime just above 2^255 rejects almost half of all tries
+    (E[tries] = 2^256/p ~ 2), so the two-pass engine's retry pass ends in
+    long chains that each wave hands to quads once its queue is drained
+    (hb_engine_tail): its tags == the oracle's, and == the queued quad engine's
+    (HB_MID_BLOCKS) on 2 M blocks.  Reference: PySwizzle.py:279-314, util.py:83-96."""
+    import random
+    pys = importlib.import_module("heartbeat_amd.PySwizzle.PySwizzle")
+    rng = random.Random(4242)
+    while True:
+        p = (1 << 255) + (rng.getrandbits(200) | 1)
+        if pys._is_probable_prime(p):
+            break
+    w = nat.width_of(p)
+    C = (p.bit_length() // 8) * S
+    nbytes = (nblocks - 1) * C + 7
+    data = np.random.default_rng(nblocks).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+    fk, ak = hashlib.sha256(b"rt-f").digest(), hashlib.sha256(b"rt-a").digest()
+    buf = DevBuf(nat, nbytes)
+    res = []
+    try:
+        buf.upload(data)
+        for mode in ("two_pass", check):
+            if mode == "two_pass":
+                monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")
+            else:
+                monkeypatch.delenv("HB_NO_SMALL_ENCODE", raising=False)
+                monkeypatch.setenv("HB_MID_BLOCKS", "100000000")
+            if mode == "oracle":
+                break
+            tb = DevBuf(nat, nblocks * w)
+            try:
+                tries = dev_encode(nat, p, S, fk, ak, buf.p, nbytes, nblocks, tb.p)
+                assert tries > 1.8 * nblocks, tries   # the retry pass had long chains to run
+                res.append(tb.download())
+            finally:
+                tb.free()
+    finally:
+        monkeypatch.delenv("HB_NO_SMALL_ENCODE", raising=False)
+        monkeypatch.delenv("HB_MID_BLOCKS", raising=False)
+        buf.free()
+    if check == "oracle":
+        assert split_tags(res[0], w) == oracle.encode(p, S, fk, ak, data, nthreads=8)
+    else:
+        assert res[0] == res[1]
