@@ -919,10 +919,14 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // vs 1.18 ms, 256 MiB 0.88 vs 1.48, 512 MiB (2^20 + 1 blocks) 1.50 vs
     // 1.63; S = 1, 2^20 + 1 blocks 1.07 vs 1.58; 1024-bit S = 10, 839 K
     // blocks 6.54 vs 8.75; but a 256-bit prime with E[tries] 1.95 at 2 M
-    // blocks 3.58 vs 3.32 (profiles/r05/mid).  $HB_MID_BLOCKS (test switch,
-    // A/B): another bound, 0 = none.
+    // blocks 3.58 vs 3.32 (profiles/r05/mid).  Wider primes keep the
+    // advantage longer (their two-pass retry chains are 2-4x longer): up to
+    // 32 x 256 x #CUs blocks for NL >= 16 -- 512-bit S = 16, 2^20 + 1 blocks
+    // 3.73 vs 5.01 ms; 1024-bit S = 10, 1.68 M blocks 11.0 vs 11.6, but 2.5 M
+    // 15.7 vs 15.3 (profiles/r05/mid/wide_*.log).  $HB_MID_BLOCKS (test
+    // switch, A/B): another bound, 0 = none.
     const char *mid_env = sw_env(c, "HB_MID_BLOCKS");
-    const u64 mid_max = mid_env ? strtoull(mid_env, nullptr, 10) : 17ull * 256ull * (u64)c->num_cus;
+    const u64 mid_max = mid_env ? strtoull(mid_env, nullptr, 10) : (NL <= 8 ? 17ull : 32ull) * 256ull * (u64)c->num_cus;
     const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max &&
                        (use_quad(c, launch_max + S) || launch_max <= mid_max) && !sw_env(c, "HB_NO_SMALL_ENCODE");
     int rc = 0;

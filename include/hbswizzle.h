@@ -122,7 +122,7 @@ const char *hb_build_flags_string(void);
 #define HB_SW_NO_VERIFY_FUSE 32768u  /* HB_NO_VERIFY_FUSE: verify as a launch sequence (PRFs, mont, hb_wsum_kernel) */
 #define HB_SW_NO_SMALL_ENCODE 65536u /* HB_NO_SMALL_ENCODE: the two-pass engine for small inputs too */
 #define HB_SW_NO_PROVE_UPLOAD 131072u /* HB_NO_PROVE_UPLOAD: small host files are gathered on the host, not uploaded */
-#define HB_SW_MID_BLOCKS 262144u     /* HB_MID_BLOCKS=n: up to n blocks per launch (default 17 x 256 x #CUs) take the queued quad-PRF + MAC path */
+#define HB_SW_MID_BLOCKS 262144u     /* HB_MID_BLOCKS=n: up to n blocks per launch (default 17 x 256 x #CUs; 32 x for primes above 256 bits) take the queued quad-PRF + MAC path */
 uint32_t hb_test_switches(void);
 
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens
