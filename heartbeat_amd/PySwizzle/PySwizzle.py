@@ -370,6 +370,10 @@ class PySwizzle(object):
 # 30.4 for the file (profiles/r05/f/probe2.log).  bench.py's host_path
 # measures both ways in every default run.
 REGISTER_KINDS = ("mmap", "bytesio", "bytes", "read")
+# hb_encode page-locks only host buffers of at least this many bytes (below
+# it the windows cost more than they save, hb_runtime.cpp); a smaller mapped
+# file is prefaulted instead (MAP_POPULATE), as without registration
+HOST_REGISTER_MIN = 32 << 20
 
 
 def encode_file(p, sectors, f_key, alpha_key, file, devices=None, register=None):
@@ -384,7 +388,11 @@ def encode_file(p, sectors, f_key, alpha_key, file, devices=None, register=None)
     fk, ak = _kb(f_key), _kb(alpha_key)
     if len(fk) != len(ak):
         raise HeartbeatError("f_key and alpha_key must have the same length")
-    fb = FileBuffer(file, populate=not register if register is not None else "mmap" not in REGISTER_KINDS)
+    if register is False or (register is None and "mmap" not in REGISTER_KINDS):
+        populate = True
+    else:
+        populate = HOST_REGISTER_MIN
+    fb = FileBuffer(file, populate=populate)
     try:
         nblocks = fb.len // C + 1
         # the tags land in the array the Tag keeps: no zero fill, no copy of
@@ -397,3 +405,11 @@ def encode_file(p, sectors, f_key, alpha_key, file, devices=None, register=None)
     finally:
         fb.close()
     return Tag._from_raw(memoryview(out), w), nblocks
+
+
+# The reference's module path (heartbeat/PySwizzle/PySwizzle.py): pickles of
+# these objects name heartbeat.PySwizzle.PySwizzle, which the repo's
+# heartbeat/ package re-exports them from, so they load under either package.
+for _c in (Challenge, Tag, State, Proof, PySwizzle):
+    _c.__module__ = "heartbeat.PySwizzle.PySwizzle"
+del _c

@@ -527,3 +527,11 @@ class Swizzle(_Serializable):
     @staticmethod
     def proof_type():
         return Proof
+
+
+# The extension module's path (cxx/Swizzle.hxx:738, imported as
+# heartbeat.Swizzle): pickles name heartbeat.Swizzle.<type>, which the repo's
+# heartbeat/ package re-exports.
+for _c in (Swizzle, Tag, State, Challenge, Proof):
+    _c.__module__ = "heartbeat.Swizzle"
+del _c

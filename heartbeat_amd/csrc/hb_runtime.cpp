@@ -1078,7 +1078,15 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             const bool placed = use_quad(c, nb + S);
             if (alpha_todo) {
                 int nra = 0;
-                if (!placed || !make_prf<NL>(a_key, key_len, p_be, p_len, F2.pa, nra) || nra != nr) {
+                // hb_prf_pair_kernel gives F and alpha 16-job wave positions
+                // of their own: ceil(nb/16) + ceil(S/16) of the grid's 16 G,
+                // which can be one more than ceil((nb + S)/16) -- with the
+                // grid capped at #CUs that last position does not exist
+                // (e.g. nb = 65535, S = 1 on 256 CUs) and alpha would never
+                // be computed.  Such a launch runs alpha on its own first.
+                const u64 pair_pos = (nb + 15) / 16 + ((u64)S + 15) / 16;
+                const bool pair_fits = pair_pos <= 16ull * (u64)quad_engine(c, nb + S).grid;
+                if (!placed || !pair_fits || !make_prf<NL>(a_key, key_len, p_be, p_len, F2.pa, nra) || nra != nr) {
                     // (a different AES key length for alpha: its own launch first)
                     rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, 0);
                     if (rc) return rc;
@@ -1572,6 +1580,10 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
         }
         const size_t words = (size_t)ncols * NL + 2;
         if (int rc = ensure_hres(c, words)) return rc;
+        // finish_sums polls this word for the new token: clear what an
+        // earlier operation left there (a fused verify keeps mu in hres, and
+        // the top limb of a small-topped prime's mu_{S-1} lands on this word)
+        c->hres[(size_t)ncols * NL + 1] = 0;
         c->sums_in_hres = true;
         c->sums_polled = true;
         PA.fuse = 1u;
@@ -1720,6 +1732,14 @@ int prove_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi
     // the finalizing launch ran to its end (its status decides rc) unless the
     // completion token says otherwise: then its PRF slots were not cleared
     c->prove_dirty = c->ctl_dirty;
+    // An uploaded host file above kGupKeep is not kept on the context (up to
+    // 4 GiB of device memory otherwise held until hb_ctx_destroy, next to the
+    // tags); its upload cost far more than the synchronize this needs.
+    constexpr size_t kGupKeep = 256ull << 20;
+    if (c->gup.n > kGupKeep) {
+        (void)hipStreamSynchronize(c->stream);
+        c->gup.release();
+    }
     if (rc) return rc;
     memcpy(mu_out, out.data(), (size_t)S * pi.tw);
     memcpy(sigma_out, out.data() + (size_t)S * pi.tw, pi.tw);
@@ -1781,6 +1801,7 @@ int verify_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
                     Limbs m = from_be(mu + (size_t)j * pi.tw, pi.tw, NL);
                     memcpy(hmu + (size_t)j * NL, m.data(), NL * 4);
                 }
+                c->hres[NL + 1] = 0;   // the polled token word (tokens are never 0)
                 make_mod<NL>(p, V.mod);
                 const Limbs &r2 = r2_of(c, p, NL);
                 for (int t = 0; t < NL; ++t) V.r2[t] = r2[t];

@@ -10,3 +10,8 @@ class HeartbeatError(Exception):
 
     def __str__(self):
         return self.message
+
+
+# the reference's module path (heartbeat/exc.py): pickles and tracebacks name
+# heartbeat.exc, which re-exports this class (the repo's heartbeat/ package)
+HeartbeatError.__module__ = "heartbeat.exc"

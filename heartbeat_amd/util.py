@@ -81,3 +81,6 @@ class KeyedPRF(object):
                                                             digs, len(xs), out))
         raw = out.raw
         return [int.from_bytes(raw[i * nb:(i + 1) * nb], "big") for i in range(len(xs))]
+
+
+KeyedPRF.__module__ = "heartbeat.util"   # the reference's path (repo heartbeat/ package)
