@@ -110,6 +110,11 @@ def parse(argv=None):
     ap.add_argument("--no-prove", action="store_true",
                     help="skip the configs[4] prove row of the default N = 1 configs[2] run")
     ap.add_argument("--prove-proofs", type=int, default=200, help="timed proofs of that row")
+    ap.add_argument("--no-wide", action="store_true",
+                    help="skip the `wide` row (PySwizzle's default 1024-bit prime, S = 10, 8 GiB) of the default "
+                         "N = 1 configs[2] run")
+    ap.add_argument("--no-configs1", action="store_true",
+                    help="skip the `configs1` row (configs[1]: 1 GiB, S = 1) of the default N = 1 configs[2] run")
     ap.add_argument("--dry-run", action="store_true",
                     help="exercise the launch / rank / timing / JSON plumbing without HIP calls (CPU tests)")
     args = ap.parse_args(argv)
@@ -477,6 +482,22 @@ def bench_encode(args, cfg, R):
         line["prove"] = prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, fk, ak,
                                   proofs=args.prove_proofs)
         line["prove"]["seconds_spent"] = round(time.perf_counter() - t, 1)
+    # the other encode shapes, on prefixes of this very file with tags of
+    # their own: PySwizzle's default prime size (1024-bit, S = 10) and
+    # configs[1] (1 GiB, S = 1); rows beside the headline, never `value`
+    if R.rank == 0 and R.world == 1 and args.config == "c3" and not cxx and len(pieces) == 1:
+        aes_rate_c3 = aes / (kernel_ms * 1e-3)
+        line["aes_g_per_s"] = round(aes_rate_c3 / 1e9, 2)
+        if not args.no_wide:
+            t = time.perf_counter()
+            line["wide"] = extra_encode_row(ctx, L, dptr, min(8 * GIB, length), 1024, 10, fk, ak, args,
+                                            steps=5, warmup=2, aes_rate_ref=aes_rate_c3)
+            line["wide"]["seconds_spent"] = round(time.perf_counter() - t, 1)
+        if not args.no_configs1:
+            t = time.perf_counter()
+            line["configs1"] = extra_encode_row(ctx, L, dptr, min(1 * GIB, length), 256, 1, fk, ak, args,
+                                                steps=20, warmup=3, aes_rate_ref=aes_rate_c3)
+            line["configs1"]["seconds_spent"] = round(time.perf_counter() - t, 1)
     # the host-memory rows come right after the device-resident ones: after
     # the CPU rows (16 threads streaming 64 GiB through host buffers) the same
     # rows measured 21-25 instead of 31-38 GiB/s for a real file
@@ -504,6 +525,114 @@ def bench_encode(args, cfg, R):
         print(json.dumps(line), flush=True)
     ctx.check(L.hb_device_free(ctx.h, dptr))
     ctx.check(L.hb_device_free(ctx.h, tptr))
+
+
+def seeded_prime(bits):
+    """The benchmark prime of a size: P256 for 256 bits (E[tries] 1.17), else
+    the first probable prime of a seeded stream (scripts/encode_rate.py's)."""
+    if bits == 256:
+        return P256
+    import importlib
+    pys = importlib.import_module("heartbeat_amd.PySwizzle.PySwizzle")
+    rng = random.Random(5000 + bits)
+    while True:
+        x = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        if pys._is_probable_prime(x):
+            return x
+
+
+def extra_encode_row(ctx, L, dptr, length, bits, S, fk, ak, args, steps, warmup, aes_rate_ref):
+    """A device-resident encode of another shape on the first `length` bytes
+    of the bench file, tags in a buffer of their own, after the timed region:
+    GiB/s over `steps` timed calls, the kernel phases (hb_last_kernel_phases),
+    PRF tries and AES per block, the AES rate against the headline kernel's
+    (`aes_rate_ref`), the HBM-roofline fraction of the file bytes, and a
+    parity sample (first / last 1,000 blocks + --parity-blocks random ones vs
+    the oracle).  Never `value`."""
+    from heartbeat_amd import _native
+    p = seeded_prime(bits)
+    pb = _native.be(p)
+    w = _native.width_of(p)
+    ss = p.bit_length() // 8
+    C = ss * S
+    nblocks = length // C + 1
+    nb_prf = (p.bit_length() + 7) // 8       # keystream bytes (AES) per PRF try
+    tptr = ctypes.c_void_p()
+    ctx.check(L.hb_device_malloc(ctx.h, nblocks * w, ctypes.byref(tptr)))
+    tries = ctypes.c_uint64()
+    ctx.prepare(p.bit_length())
+    try:
+        def one():
+            ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, len(fk), 0, dptr, length, nblocks, tptr, 3,
+                                  ctypes.byref(tries)))
+            return ctx.last_kernel_ms()[0], ctx.last_kernel_phases(), tries.value
+
+        for _ in range(warmup):
+            one()
+        t0 = time.perf_counter()
+        runs = [one() for _ in range(steps)]
+        el = time.perf_counter() - t0
+        kms = sum(r[0] for r in runs) / steps
+        ph = [round(sum(r[1][k] for r in runs) / steps, 4) for k in range(len(runs[0][1]))]
+        tr = sum(r[2] for r in runs) / steps
+        # the first 4 keystream bytes of every first try come from the prefix
+        # image, built once per call (2^24 + 2^16 + 2^8 byte-0 AES)
+        two_pass = len(ph) == 4
+        aes_prf = tr * nb_prf - (4 * nblocks if two_pass else 0)
+        aes_all = aes_prf + ((1 << 24) + (1 << 16) + (1 << 8) if two_pass else 0)
+        row = {"workload": "%d-bit seeded prime, %d sector%s/block (%d-byte sectors), %.3g GiB device-resident "
+                           "prefix of the bench file" % (bits, S, "s" if S > 1 else "", ss, length / GIB),
+               "prime": hex(p), "expected_tries_per_prf": round((1 << p.bit_length()) / p, 4),
+               "file_bytes": length, "blocks": nblocks,
+               "value": round(length * steps / GIB / el, 3), "unit": "GiB/s",
+               "ms_per_step": round(el / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+               "kernel_ms": round(kms, 3),
+               "kernel_gib_s": round(length / GIB / (kms * 1e-3), 3),
+               "roofline": {"bound": "hbm", "achieved": round(length / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(length / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+               "prf_tries_per_block": round(tr / nblocks, 4),
+               "aes_per_block": round(aes_all / nblocks, 3),
+               "aes_g_per_s": round(aes_all / (kms * 1e-3) / 1e9, 2),
+               "aes_rate_vs_headline_kernel": round(aes_all / (kms * 1e-3) / aes_rate_ref, 4),
+               "note": "after the timed region; never `value`"}
+        if two_pass:
+            row["phases_ms"] = {"setup (prefix image, MAC tables)": ph[0], "first_pass": ph[1], "retry_pass": ph[2],
+                                "wide_mac (hb_wmac_kernel)": ph[3]}
+            row["prf_pass_aes_g_per_s"] = round(aes_prf / ((ph[1] + ph[2]) * 1e-3) / 1e9, 2)
+        if not args.no_parity_sample:
+            row["parity_sample"] = row_parity(ctx, L, dptr, tptr, length, nblocks, S, p, fk, ak, C, w,
+                                              args.parity_blocks)
+    finally:
+        ctx.check(L.hb_device_free(ctx.h, tptr))
+    return row
+
+
+def row_parity(ctx, L, dptr, tptr, length, nblocks, S, p, fk, ak, C, w, nrand):
+    """First / last 1,000 blocks (the short tail block included) and `nrand`
+    random ones of a one-piece encode vs the oracle."""
+    import numpy as np
+    from oracle import oracle as O
+    rng = random.Random(0xC0FFEE + C)
+    picks = set(range(min(1000, nblocks))) | set(range(max(0, nblocks - 1000), nblocks))
+    while len(picks) < min(nblocks, nrand + 2000):
+        picks.add(rng.randrange(nblocks))
+    picks = sorted(picks)
+    tags = np.empty(nblocks * w, dtype=np.uint8)
+    ctx.check(L.hb_memcpy(ctx.h, tags.ctypes.data, tptr.value, nblocks * w, 2))
+    ok, i = True, 0
+    while i < len(picks):
+        j = i
+        while j + 1 < len(picks) and picks[j + 1] == picks[j] + 1:
+            j += 1
+        r0, r1 = picks[i], picks[j] + 1
+        lo, hi = r0 * C, min(r1 * C, length)
+        data = np.empty(max(hi - lo, 0), dtype=np.uint8)
+        if hi > lo:
+            ctx.check(L.hb_memcpy(ctx.h, data.ctypes.data, dptr.value + lo, hi - lo, 2))
+        want = O.encode(p, S, fk, ak, data, block_base=r0, nblocks=r1 - r0, nthreads=4)
+        ok = ok and tags[r0 * w:r1 * w].tobytes() == b"".join(t.to_bytes(w, "big") for t in want)
+        i = j + 1
+    return {"n": len(picks), "ok": ok, "what": "first/last 1,000 + %d random blocks vs oracle/swizzle_oracle.c" % nrand}
 
 
 def sustained(args, R, step, sec_per_step, file_len):

@@ -77,6 +77,8 @@ SIGNATURES = [
     ("hb_ctx_set_stream", _c.c_int, [_P, _P]),
     ("hb_ctx_wait", _c.c_int, [_P, _c.POINTER(_c.c_uint64)]),
     ("hb_ctx_prepare", _c.c_int, [_P, _c.c_uint32]),
+    ("hb_ctx_num_cus", _c.c_int, [_P, _c.POINTER(_c.c_int)]),
+    ("hb_last_kernel_phases", _c.c_int, [_P, _c.POINTER(_c.c_double), _c.c_uint32]),
     ("hb_merkle_offsets", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint64, _c.c_uint64, _c.c_uint64, _P]),
     ("hb_merkle_chunk_hmacs", _c.c_int, [_P, _B, _c.c_size_t, _c.c_uint64, _P, _c.c_uint64, _P,
                                          _c.c_uint64, _P]),
@@ -183,6 +185,22 @@ class Context(object):
             return
         with self.lock:
             self.check(L.hb_ctx_prepare(self.h, int(prime_bits)))
+
+    def last_kernel_phases(self):
+        """[set-up, first pass, retry pass, wide MAC] ms of the last
+        device-resident two-pass encode (hb_last_kernel_phases), or []."""
+        ms = (ctypes.c_double * 4)()
+        with self.lock:
+            n = lib().hb_last_kernel_phases(self.h, ms, 4)
+        if n < 0:
+            self.check(n)
+        return [round(ms[k], 4) for k in range(n)]
+
+    def num_cus(self):
+        """Compute units of the context's GPU (hb_ctx_num_cus)."""
+        n = ctypes.c_int()
+        self.check(lib().hb_ctx_num_cus(self.h, ctypes.byref(n)))
+        return n.value
 
     def last_kernel_ms(self):
         ms = ctypes.c_double()

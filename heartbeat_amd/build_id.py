@@ -12,6 +12,7 @@ Command line (used by the Makefile):
   python3 build_id.py digest FILE...      SHA-256 over the named files (+ $HB_ID_FLAGS)
   python3 build_id.py id                  the library id for $HB_ID_FLAGS
   python3 build_id.py stamp PATH VALUE    write VALUE to PATH unless it already holds it
+  python3 build_id.py stamp-digest PATH FILE...   stamp PATH with the digest of FILE...
 """
 import hashlib
 import os
@@ -61,8 +62,15 @@ def main(argv):
         print(library_id(digest_files(named), flags))
     elif argv[:1] == ["id"]:
         print(library_id(sources_digest(), flags))
-    elif argv[:1] == ["stamp"] and len(argv) == 3:
-        path, value = argv[1], argv[2]
+    elif argv[:1] in (["stamp"], ["stamp-digest"]) and len(argv) >= 3:
+        path = argv[1]
+        if argv[0] == "stamp-digest":
+            value = library_id(digest_files([(os.path.basename(p), p) for p in argv[2:]]), flags)
+        elif len(argv) == 3:
+            value = argv[2]
+        else:
+            sys.stderr.write(__doc__)
+            return 2
         try:
             with open(path) as fh:
                 if fh.read().strip() == value:

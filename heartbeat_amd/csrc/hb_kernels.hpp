@@ -384,7 +384,10 @@ __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const Prf
 // the quad engine's round (hb_quad_prf_try: ~147 clocks per AES round against
 // ~300 for a lone lane running all 16 lookups).  The pass ends on its longest
 // chains, so this halves its tail.  The quads' accept runs the block's
-// finish on one lane (the MFMA path's partial sum + F: cheap at NL = 8).
+// finish on one lane (the MFMA path's partial sum + F: cheap at NL = 8; the
+// split wide-prime encode's F store, ALIGN = 0).  The wide primes need it
+// most: a 1024-bit try is 128 serial AES, and the longest of ~3 M retry
+// chains runs ~17 tries.
 #ifndef HB_RETRY_QUAD_TAIL
 #define HB_RETRY_QUAD_TAIL 1
 #endif
@@ -496,9 +499,22 @@ struct HbEncodeOcc { static constexpr int v = NL <= 8 ? HB_OCC8 : 1; };
 #endif
 template <int NL>
 struct HbEncodeWg { static constexpr int v = NL >= HB_WIDE_NL ? HB_WIDE_WG : HB_ENGINE_WG; };
+// ALIGN = 0: the split wide-prime encode's PRF passes, which only store F
+// (the MAC is hb_wmac_kernel's): no MAC accumulator, so 1,024-thread
+// workgroups at every prime size -- 16 waves per CU on one LDS table image,
+// the 256-bit kernel's occupancy
+template <int NL, int ALIGN>
+struct HbEncWg { static constexpr int v = ALIGN == 0 ? HB_ENGINE_WG : HbEncodeWg<NL>::v; };
 
 
 __device__ __forceinline__ void hb_zero_sr(u32 sr[4]) { sr[0] = sr[1] = sr[2] = sr[3] = 0; }
+
+// NL little-endian limbs to 16-byte aligned global memory (NL % 4 == 0)
+template <int NL>
+__device__ __forceinline__ void hb_store_limbs(u32 *dst, const u32 v[NL]) {
+    HB_UNROLL
+    for (int t = 0; t < NL; t += 4) *reinterpret_cast<uint4 *>(dst + t) = make_uint4(v[t], v[t + 1], v[t + 2], v[t + 3]);
+}
 
 template <int NL, int ALIGN, int MODE = 0>
 struct EncodeHandler {
@@ -506,24 +522,28 @@ struct EncodeHandler {
     __device__ __forceinline__ u64 x_of(u64 job) const { return A.block_base + job; }
     __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
     __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
+        if constexpr (ALIGN == 0) {   // split wide-prime encode: F for hb_wmac_kernel
+            hb_store_limbs<NL>(A.fout + job * NL, F);
+        } else {
 #if defined(HB_EXP_NO_MAC)
-        hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, F);
-#else
-        if (MODE == 1 && job * A.C >= A.len) {
-            // cxx: no sector read -> sigma = f(chunk_id) without `%= p`
-            // (shacham_waters_private.cxx:681-690; differs only if F >= p)
             hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, F);
-            return;
-        }
-        u32 tag[NL];
-        hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
-        hb_store_tag<NL, ALIGN>(A.tags + job * (u64)A.tw, A.tw, tag);
+#else
+            if (MODE == 1 && job * A.C >= A.len) {
+                // cxx: no sector read -> sigma = f(chunk_id) without `%= p`
+                // (shacham_waters_private.cxx:681-690; differs only if F >= p)
+                hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, F);
+                return;
+            }
+            u32 tag[NL];
+            hb_block_tag<NL, ALIGN>(A.data, A.len, job, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
+            hb_store_tag<NL, ALIGN>(A.tags + job * (u64)A.tw, A.tw, tag);
 #endif
+        }
     }
 };
 
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_encode_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__((HbEncWg<NL, ALIGN>::v), HbEncodeOcc<NL>::v) void hb_encode_kernel(EncodeArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
@@ -602,7 +622,7 @@ __global__ __launch_bounds__(HbMacSplit<NL>::T) void hb_mac_split_kernel(EncodeA
 // engine and MAC with the cxx prf (CFB-128: nb/16 full AES per try instead of
 // nb byte-0 AES).
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_cxx_encode_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__((HbEncWg<NL, ALIGN>::v), HbEncodeOcc<NL>::v) void hb_cxx_encode_kernel(EncodeArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
@@ -1076,7 +1096,7 @@ __device__ __forceinline__ void hb_first_finish(const EncodeArgs<NL> &A, const L
 }
 
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__((HbEncWg<NL, ALIGN>::v), HbEncodeOcc<NL>::v) void hb_encode_first_kernel(EncodeArgs<NL> A) {
     // MFMA MAC for 256-bit primes with aligned full-width sectors (A.mfma set by the host)
     constexpr bool MF = NL == 8 && ALIGN == 16;
     // MF: the T-table image plus the MFMA A fragments (HB_MFMA_NT x S x 1 KiB,
@@ -1171,6 +1191,10 @@ struct RetryHandler {
 #endif
     __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
         const u64 blk = A.retry[job].blk;
+        if constexpr (ALIGN == 0) {   // split wide-prime encode: F for hb_wmac_kernel
+            hb_store_limbs<NL>(A.fout + blk * NL, F);
+            return;
+        } else {
         u32 tag[NL];
         if (NL == 8 && A.mfma) {
             // the first pass left sum_j alpha_j m_j mod p: tag = (F + part) mod p
@@ -1187,11 +1211,12 @@ struct RetryHandler {
             hb_block_tag<NL, ALIGN>(A.data, A.len, blk, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
         }
         hb_store_tag<NL, ALIGN>(A.tags + blk * (u64)A.tw, A.tw, tag);
+        }
     }
 };
 
 template <int NL, int NR, int ALIGN>
-__global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_encode_retry_kernel(EncodeArgs<NL> A) {
+__global__ __launch_bounds__((HbEncWg<NL, ALIGN>::v), HbEncodeOcc<NL>::v) void hb_encode_retry_kernel(EncodeArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) u32 lds[HB_LDS_WORDS];
     // pass 1 has completed (stream order): the count is final
     const u64 cnt = *(volatile unsigned long long *)A.retry_count;
@@ -1200,8 +1225,23 @@ __global__ __launch_bounds__(HbEncodeWg<NL>::v, HbEncodeOcc<NL>::v) void hb_enco
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     RetryHandler<NL, ALIGN> h{A};
-    if constexpr (NL == 8 && HB_RETRY_QUAD_TAIL) hb_engine_tail<NL, NR>(h, L, A.prf, n, A.queue);
+    if constexpr ((NL == 8 || ALIGN == 0) && HB_RETRY_QUAD_TAIL) hb_engine_tail<NL, NR>(h, L, A.prf, n, A.queue);
     else hb_engine<NL, NR>(h, L, A.prf, n, A.queue);
+}
+
+// r (NL limbs, < p) += x (NL limbs, < p) mod p
+template <int NL>
+__device__ __forceinline__ void hb_add_mod(u32 r[NL], const u32 *x, const ModP<NL> &M) {
+    u32 v[NL + 1], o[NL];
+    u64 c = 0;
+    for (int t = 0; t < NL; ++t) {
+        c += (u64)r[t] + x[t];
+        v[t] = (u32)c;
+        c >>= 32;
+    }
+    v[NL] = (u32)c;
+    hb_reduce_small<NL>(v, M, o);
+    for (int t = 0; t < NL; ++t) r[t] = o[t];
 }
 
 // ------------------------------------------------------------------ PRF batch
@@ -1900,21 +1940,6 @@ __device__ __forceinline__ void hb_sector_value(const unsigned char *data, u64 l
     }
 }
 
-// r (NL limbs, < p) += x (NL limbs, < p) mod p
-template <int NL>
-__device__ __forceinline__ void hb_add_mod(u32 r[NL], const u32 *x, const ModP<NL> &M) {
-    u32 v[NL + 1], o[NL];
-    u64 c = 0;
-    for (int t = 0; t < NL; ++t) {
-        c += (u64)r[t] + x[t];
-        v[t] = (u32)c;
-        c >>= 32;
-    }
-    v[NL] = (u32)c;
-    hb_reduce_small<NL>(v, M, o);
-    for (int t = 0; t < NL; ++t) r[t] = o[t];
-}
-
 // sh[k*(NL+1) ..]: n values of NL+1 limbs (whose total fits NL+1 limbs);
 // leaves their sum in sh[0 .. NL].  Block-wide call.
 template <int NL>
@@ -2104,15 +2129,25 @@ __host__ inline void hb_load_kernel(K *k) {
 // 3 = cxx prf encode
 template <int NL, int PASS>
 hipError_t hb_launch_encode_pass(const EncodeArgs<NL> &A, int nr, int align, int grid, hipStream_t s) {
-    dim3 g(grid), b(HbEncodeWg<NL>::v);
-#define HB_ENC(K, NRV, AL) HB_LAUNCH((K<NL, NRV, AL>), g, b, s, A)
+    dim3 g(grid);
+#define HB_ENC(K, NRV, AL) HB_LAUNCH((K<NL, NRV, AL>), g, dim3(HbEncWg<NL, AL>::v), s, A)
 #define HB_ENC_NR(K, AL) \
     do { if (nr == 14) HB_ENC(K, 14, AL); else if (nr == 12) HB_ENC(K, 12, AL); else HB_ENC(K, 10, AL); } while (0)
 #define HB_ENC_AL(K) do { if (align == 16) HB_ENC_NR(K, 16); else HB_ENC_NR(K, 1); } while (0)
-    if constexpr (PASS == 1) HB_ENC_AL(hb_encode_first_kernel);
-    else if constexpr (PASS == 2) HB_ENC_AL(hb_encode_retry_kernel);
+    // align 0: the split wide-prime encode's F-only passes (NL >= 16)
+#define HB_ENC_AL0(K)                                              \
+    do {                                                           \
+        if constexpr (NL >= 16) {                                  \
+            if (align == 0) { HB_ENC_NR(K, 0); break; }            \
+        }                                                          \
+        if (align == 0) return hipErrorInvalidValue;               \
+        HB_ENC_AL(K);                                              \
+    } while (0)
+    if constexpr (PASS == 1) HB_ENC_AL0(hb_encode_first_kernel);
+    else if constexpr (PASS == 2) HB_ENC_AL0(hb_encode_retry_kernel);
     else if constexpr (PASS == 3) HB_ENC_AL(hb_cxx_encode_kernel);
     else HB_ENC_AL(hb_encode_kernel);
+#undef HB_ENC_AL0
 #undef HB_ENC_AL
 #undef HB_ENC_NR
 #undef HB_ENC

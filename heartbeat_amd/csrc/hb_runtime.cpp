@@ -43,6 +43,8 @@ hipError_t hb_launch_fill(unsigned char *, u64, u64, hipStream_t);
 hipError_t hb_launch_read(const void *, u64, u32 *, int, hipStream_t);
 hipError_t hb_launch_merkle_offsets(const MerkleArgs &, int, hipStream_t);
 hipError_t hb_launch_hmac(const MerkleArgs &, hipStream_t);
+template <int NL> hipError_t hb_launch_wtab(const WtabArgs<NL> &, hipStream_t);
+template <int NL> hipError_t hb_launch_wmac(const WmacArgs<NL> &, hipStream_t);
 
 namespace {
 
@@ -94,6 +96,10 @@ struct hb_ctx {
     int num_cus = 256;
     hipStream_t stream = nullptr, copy = nullptr;
     hipEvent_t k0 = nullptr, k1 = nullptr;
+    // phase marks of a device-resident two-pass encode (hb_last_kernel_phases):
+    // after the set-up kernels, after the first pass, after the retry pass
+    hipEvent_t ph[3] = {nullptr, nullptr, nullptr};
+    bool ph_valid = false;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
     u32 *t0 = nullptr;
     unsigned long long *queue = nullptr;   // 16 slots of HB_QSLOT counters
@@ -105,6 +111,9 @@ struct hb_ctx {
     DevBuf gdev;         // device-resident prove: the challenged blocks and tags, gathered
     DevBuf facc;         // fused prove: per-column limb sums over workgroups (zero between operations)
     DevBuf gup;          // prove of a small host file: the file, uploaded whole
+    DevBuf wpw;          // split wide-prime encode: 256^e mod p, e < ss (for wide_key)
+    DevBuf wtab;         // its digit table (A fragments), kz, status word
+    Limbs wide_key;      // p of wpw, then ss (wide_prep)
     HostBuf gstage[2];   // host-file prove: pinned gather buffers (blocks | tags), double-buffered
     HostBuf hscratch;    // pinned staging of the encode's small host round trips (alpha, MFMA tables)
     // the alpha D2H into hscratch done / the MFMA-table H2D out of it done
@@ -199,6 +208,7 @@ const SwitchName kSwitches[] = {
     {"HB_NO_SMALL_ENCODE", HB_SW_NO_SMALL_ENCODE},
     {"HB_NO_PROVE_UPLOAD", HB_SW_NO_PROVE_UPLOAD},
     {"HB_MID_BLOCKS", HB_SW_MID_BLOCKS},
+    {"HB_NO_WIDE", HB_SW_NO_WIDE},
 };
 
 int nl_for_bits(int bits) {
@@ -386,6 +396,15 @@ void prepare_nl(hb_ctx *c) {
     memset(&E, 0, sizeof E);
     for (int pass = 0; pass <= 3; ++pass)
         for (int align : {16, 1}) (void)hb_launch_encode<NL>(E, 14, align, pass, 0, c->stream);
+    if constexpr (NL >= 16) {   // the split wide-prime encode (wide_plan)
+        for (int pass = 1; pass <= 2; ++pass) (void)hb_launch_encode<NL>(E, 14, 0, pass, 0, c->stream);
+        WtabArgs<NL> WT;
+        memset(&WT, 0, sizeof WT);
+        (void)hb_launch_wtab<NL>(WT, c->stream);
+        WmacArgs<NL> WM;
+        memset(&WM, 0, sizeof WM);
+        (void)hb_launch_wmac<NL>(WM, c->stream);
+    }
     for (int align : {16, 1}) (void)hb_launch_mac<NL>(E, align, c->stream);
     Prf2Args<NL> P2;
     memset(&P2, 0, sizeof P2);
@@ -880,6 +899,74 @@ void settle(hb_ctx *c) {
     done(check_prf_slots(c));
 }
 
+// ------------------------------------------------------------------ split wide-prime encode
+// Primes above 256 bits (NL >= 16), PySwizzle PRF, two-pass: the first-try
+// and retry passes store F only (ALIGN = 0, 1,024-thread workgroups), and the
+// sector MAC runs on the int8 matrix cores (hb_wide.hpp): a digit table built
+// on the device from alpha (hb_wtab_kernel), then per launch hb_wmac_kernel
+// (whole blocks) and hb_wmac_tail_kernel (the short last block, VALU).
+// Applies when C % 16 == 0 (16-byte block loads), C <= HB_WIDE_MAX_C and w
+// (below) <= 29; $HB_NO_WIDE (test switch, A/B): the in-kernel VALU MAC.
+//
+// w: the smallest shift with p 2^w > C 128 2^(8D - 1) >= |sum_x r'_x (u_x -
+// 128)| (|r'_x| <= 2^(8D-1)), so that T = sum_c col_c 256^c + kz > 0; then
+// T < 3 p 2^w and T + F < 2^32 p, the range of hb_reduce_small; the column
+// sums |col_c| <= C 2^14 stay inside int32 for C <= HB_WIDE_MAX_C.
+template <int NL>
+bool wide_plan(const PrimeInfo &pi, u64 C, WtabArgs<NL> &W, u32 &w_out) {
+    if (C == 0 || C % 16 != 0 || C > HB_WIDE_MAX_C) return false;
+    const u32 D = pi.tw;
+    int lc = 0;
+    while ((1ull << lc) < C) ++lc;   // ceil(log2 C)
+    const int w = lc + 8 * (int)D + 7 - pi.bits;
+    if (w < 0 || w > 29) return false;
+    W.C = (u32)C;
+    W.ss = pi.ss;
+    W.D = D;
+    W.Mt = (D + 15) / 16;
+    W.nslices = (u32)((C + 63) / 64);
+    if ((int)W.Mt > NL / 4) return false;
+    for (int t = 0; t < NL; ++t) W.half[t] = 0;
+    for (u32 i = 0; i < D; ++i) W.half[i / 4] |= 0x7fu << (8 * (i % 4));
+    w_out = (u32)w;
+    return true;
+}
+
+// The tables of wide_plan that depend on p and ss only -- 256^e mod p (e <
+// ss, uploaded to c->wpw) and 128 G mod p, G = sum_e 256^e -- rebuilt when p
+// or ss changes; p 2^w into W.p2w.
+template <int NL>
+int wide_prep(hb_ctx *c, const Limbs &p, const PrimeInfo &pi, u32 w, WtabArgs<NL> &W) {
+    Limbs key(p);
+    key.push_back(pi.ss);
+    if (key != c->wide_key) {
+        std::vector<u32> pw((size_t)pi.ss * NL, 0);
+        Limbs x(NL, 0), g(NL, 0);
+        x[0] = 1;
+        if (cmp(x, p) >= 0) x = mod_any(x, p);
+        for (u32 e = 0; e < pi.ss; ++e) {
+            for (int t = 0; t < NL; ++t) pw[(size_t)e * NL + t] = x[t];
+            g = add_mod(g, x, p);
+            for (int b = 0; b < 8; ++b) x = add_mod(x, x, p);   // x = 256 x mod p
+        }
+        for (int b = 0; b < 7; ++b) g = add_mod(g, g, p);       // 128 G mod p
+        HB_CHECK(c->wpw.ensure(pw.size() * 4), "hipMalloc(wide pw)");
+        HB_CHECK(hipStreamSynchronize(c->stream), "hipStreamSynchronize");   // an earlier table build may read wpw
+        HB_CHECK(hipMemcpy(c->wpw.p, pw.data(), pw.size() * 4, hipMemcpyHostToDevice), "H2D(wide pw)");
+        c->wide_key = key;
+        c->wide_key.insert(c->wide_key.end(), g.begin(), g.end());   // cached 128 G mod p
+    }
+    for (int t = 0; t < NL; ++t) W.g128[t] = c->wide_key[c->wide_key.size() - NL + t];
+    // p 2^w, NL + 1 limbs
+    for (int t = 0; t <= NL; ++t) {
+        const u64 lo = t < NL ? (u64)p[t] << w : 0u;
+        const u64 hi = t >= 1 && w ? (u64)p[t - 1] >> (32 - w) : 0u;
+        W.p2w[t] = (u32)(lo | hi);
+    }
+    W.pw = (const u32 *)c->wpw.p;
+    return 0;
+}
+
 template <int NL>
 int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &pi, u32 S,
                 const uint8_t *f_key, const uint8_t *a_key, size_t key_len, u64 block_base,
@@ -991,13 +1078,13 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     HB_CHECK(hipMemsetAsync(q7, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
 
     const bool tags_dev = flags & HB_TAGS_ON_DEVICE;
+    const bool data_dev = flags & HB_DATA_ON_DEVICE;
     uint8_t *dtags = tags;
     if (!tags_dev) {
         HB_CHECK(c->tags.ensure((size_t)(nblocks * pi.tw)), "hipMalloc(tags)");
         dtags = (uint8_t *)c->tags.p;
     }
     // Host bytes go through the GPU in chunks of cb whole blocks.
-    const bool data_dev = flags & HB_DATA_ON_DEVICE;
     u64 cb = C ? (256ull << 20) / C : 1;
     if (cb < 1) cb = 1;
     const u64 launch_blocks = data_dev ? nblocks : (nblocks < cb ? nblocks : cb);
@@ -1009,6 +1096,31 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     if (small) {
         HB_CHECK(c->vals.ensure((size_t)launch_blocks * NL * 4), "hipMalloc(F)");
         A.fv = (const u32 *)c->vals.p;
+    }
+    // split wide-prime encode (wide_plan): F into the tag slots when they are
+    // exactly NL limbs wide and 16-byte aligned, else into c->vals
+    WtabArgs<NL> WT;
+    memset(&WT, 0, sizeof WT);
+    bool wide = false;
+    bool f_in_tags = false;
+    if constexpr (NL >= 16) {
+        u32 w = 0;
+        wide = two_pass && !cxx && (!data_dev || (uintptr_t)data % 16 == 0) && wide_plan<NL>(pi, C, WT, w) &&
+               !sw_env(c, "HB_NO_WIDE");
+        if (wide) {
+            if (int rc2 = wide_prep<NL>(c, p, pi, w, WT)) return rc2;
+            const size_t fbytes = (size_t)WT.nslices * WT.Mt * 64 * 16;
+            HB_CHECK(c->wtab.ensure(fbytes + (size_t)(NL + 1) * 4 + 16), "hipMalloc(wide table)");
+            WT.mod = A.mod;
+            WT.S = S;
+            WT.alpha_mont = (const u32 *)c->alpha_mont.p;
+            WT.afrag = (int8_t *)c->wtab.p;
+            WT.kz = (u32 *)((uint8_t *)c->wtab.p + fbytes);
+            WT.status = (unsigned int *)(WT.kz + NL + 1);
+            f_in_tags = pi.tw == 4u * NL && (uintptr_t)dtags % 16 == 0;
+            if (!f_in_tags) HB_CHECK(c->vals.ensure((size_t)launch_blocks * NL * 4), "hipMalloc(F)");
+            mark("wide tables");
+        }
     }
     if (two_pass) {
         A.retry_cap = retry_capacity(c, p_be, p_len, launch_blocks);
@@ -1034,6 +1146,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         if (rc) return rc;
     }
     c->last_launches = 0;
+    c->ph_valid = false;
     float ms_total = 0.f;
     // the prefix image is part of the encode (rebuilt for every f_key): timed
     HB_CHECK(hipEventRecord(c->k0, c->stream), "hipEventRecord");
@@ -1043,6 +1156,12 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         PA.t0 = c->t0;
         PA.out = (unsigned char *)c->pfx.p;
         HB_CHECK(hb_launch_prefix(PA, nr, c->num_cus, c->stream), "hb_prefix_kernel launch");
+        c->last_launches++;
+    }
+    if (wide) {
+        // the digit table and kz from alpha_j R mod p (on the device, in stream order)
+        HB_CHECK(hipMemsetAsync(WT.status, 0, 4, c->stream), "hipMemsetAsync");
+        HB_CHECK(hb_launch_wtab<NL>(WT, c->stream), "hb_wtab_kernel launch");
         c->last_launches++;
     }
     if (mf_layout) {
@@ -1130,13 +1249,43 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         }
         HB_CHECK(hipMemsetAsync(q0 + 3, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
         A.queue = q0;
-        HB_CHECK(hb_launch_encode<NL>(A, nr, align, 1, engine_grid(c, nb), c->stream),
+        if (data_dev) HB_CHECK(hipEventRecord(c->ph[0], c->stream), "hipEventRecord");
+        const int palign = wide ? 0 : align;
+        if (wide) A.fout = f_in_tags ? (u32 *)tg : (u32 *)c->vals.p;
+        HB_CHECK(hb_launch_encode<NL>(A, nr, palign, 1, engine_grid(c, nb), c->stream),
                  "hb_encode_first_kernel launch");
+        if (data_dev) HB_CHECK(hipEventRecord(c->ph[1], c->stream), "hipEventRecord");
         HB_CHECK(hipMemsetAsync(q7, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
         A.queue = q7;
-        HB_CHECK(hb_launch_encode<NL>(A, nr, align, 2, engine_grid(c, A.retry_cap), c->stream),
+        HB_CHECK(hb_launch_encode<NL>(A, nr, palign, 2, engine_grid(c, A.retry_cap), c->stream),
                  "hb_encode_retry_kernel launch");
+        if (data_dev) HB_CHECK(hipEventRecord(c->ph[2], c->stream), "hipEventRecord");
+        c->ph_valid = data_dev;
         c->last_launches += 2;
+        if constexpr (NL >= 16) {
+            if (wide) {
+                WmacArgs<NL> M;
+                memset(&M, 0, sizeof M);
+                M.mod = A.mod;
+                M.data = d;
+                M.len = dlen;
+                M.nblocks = nb;
+                M.nfull = dlen / C < nb ? dlen / C : nb;
+                M.C = C;
+                M.ss = pi.ss;
+                M.S = S;
+                M.tw = pi.tw;
+                M.Mt = WT.Mt;
+                M.nslices = WT.nslices;
+                M.afrag = WT.afrag;
+                M.kz = WT.kz;
+                M.fsrc = A.fout;
+                M.tags = tg;
+                M.alpha_mont = (const u32 *)c->alpha_mont.p;
+                HB_CHECK(hb_launch_wmac<NL>(M, c->stream), "hb_wmac_kernel launch");
+                c->last_launches += (M.nfull ? 1 : 0) + (nb > M.nfull ? 1 : 0);
+            }
+        }
         return 0;
     };
 
@@ -1236,6 +1385,11 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     HB_CHECK(hipMemcpy(qs, c->queue, sizeof qs, hipMemcpyDeviceToHost), "hipMemcpy(queue)");
     const unsigned long long *q = qs, *r = qs + HB_QSLOT * HB_SLOT_RETRY;
     if (q[2] || r[2]) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate for some blocks");
+    if (wide) {
+        u32 st = 0;
+        HB_CHECK(hipMemcpy(&st, WT.status, 4, hipMemcpyDeviceToHost), "hipMemcpy(status)");
+        if (st) return fail(c, HB_EHIP, "internal: wide MAC digit table did not close");
+    }
     if (tries_out) *tries_out = q[1] + r[1];
     for (int s = 0; s < 16; ++s)
         if (qs[s * HB_QSLOT + 2]) return fail(c, HB_EINVAL, "PRF rejection sampling did not terminate");
@@ -1964,6 +2118,8 @@ int hb_ctx_create(int device, hb_ctx **out) {
     if ((e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
     if ((e = hipEventCreate(&c->k0)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreate(&c->k1)) != hipSuccess) return bad(e, "hipEventCreate");
+    for (int k = 0; k < 3; ++k)
+        if ((e = hipEventCreate(&c->ph[k])) != hipSuccess) return bad(e, "hipEventCreate");
     for (int b = 0; b < 2; ++b) {
         if ((e = hipEventCreateWithFlags(&c->copied[b], hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
         if ((e = hipEventCreateWithFlags(&c->done[b], hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
@@ -1991,7 +2147,7 @@ void hb_ctx_destroy(hb_ctx *c) {
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
                       &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
                       &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig, &c->gdev,
-                      &c->facc, &c->gup};
+                      &c->facc, &c->gup, &c->wpw, &c->wtab};
     for (DevBuf *b : bufs) b->release();
     if (c->hres) (void)hipHostFree(c->hres);
     c->gstage[0].release();
@@ -2001,6 +2157,8 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->queue) (void)hipFree(c->queue);
     if (c->k0) (void)hipEventDestroy(c->k0);
     if (c->k1) (void)hipEventDestroy(c->k1);
+    for (int k = 0; k < 3; ++k)
+        if (c->ph[k]) (void)hipEventDestroy(c->ph[k]);
     if (c->ev_alpha) (void)hipEventDestroy(c->ev_alpha);
     if (c->ev_h2d) (void)hipEventDestroy(c->ev_h2d);
     for (int b = 0; b < 2; ++b) {
@@ -2010,6 +2168,27 @@ void hb_ctx_destroy(hb_ctx *c) {
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
     delete c;
+}
+
+int hb_last_kernel_phases(hb_ctx *c, double *ms, uint32_t n) {
+    if (!c || (!ms && n)) return HB_EINVAL;
+    settle(c);
+    if (!c->ph_valid || n == 0) return 0;
+    hipEvent_t ev[5] = {c->k0, c->ph[0], c->ph[1], c->ph[2], c->k1};
+    HB_CHECK(hipEventSynchronize(c->k1), "hipEventSynchronize");
+    uint32_t k = 0;
+    for (; k < 4 && k < n; ++k) {
+        float f = 0.f;
+        HB_CHECK(hipEventElapsedTime(&f, ev[k], ev[k + 1]), "hipEventElapsedTime");
+        ms[k] = f;
+    }
+    return (int)k;
+}
+
+int hb_ctx_num_cus(const hb_ctx *c, int *out) {
+    if (!c || !out) return HB_EINVAL;
+    *out = c->num_cus;
+    return 0;
 }
 
 int hb_ctx_set_stream(hb_ctx *c, void *stream) {

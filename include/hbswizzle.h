@@ -123,6 +123,7 @@ const char *hb_build_flags_string(void);
 #define HB_SW_NO_SMALL_ENCODE 65536u /* HB_NO_SMALL_ENCODE: the two-pass engine for small inputs too */
 #define HB_SW_NO_PROVE_UPLOAD 131072u /* HB_NO_PROVE_UPLOAD: small host files are gathered on the host, not uploaded */
 #define HB_SW_MID_BLOCKS 262144u     /* HB_MID_BLOCKS=n: up to n blocks per launch (default 17 x 256 x #CUs; 32 x for primes above 256 bits) take the queued quad-PRF + MAC path */
+#define HB_SW_NO_WIDE 524288u       /* HB_NO_WIDE: primes above 256 bits keep the MAC inside the PRF kernels (VALU) instead of the split F-only passes + MFMA MAC (hb_wmac_kernel) */
 uint32_t hb_test_switches(void);
 
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens
@@ -142,6 +143,11 @@ void hb_ctx_destroy(hb_ctx *ctx);
 /* Message of the last error on this context (or of the last failed
  * hb_ctx_create when ctx is NULL). */
 const char *hb_last_error(const hb_ctx *ctx);
+
+/* Compute units of the context's device (the small-input encode and the
+ * prove size their launches by it; tests place inputs at those limits).
+ * Replaces nothing in the reference. */
+int hb_ctx_num_cus(const hb_ctx *ctx, int *out);
 
 /* Enqueue this context's kernels on `stream` (a hipStream_t of the
  * context's device, e.g. torch.cuda.current_stream().cuda_stream), or on the
@@ -311,6 +317,15 @@ int hb_aes_cfb128(const uint8_t *key, size_t key_len, const uint8_t *iv,
  * pending HB_ASYNC encode is completed first (its status stays for
  * hb_ctx_wait). */
 int hb_last_kernel_ms(hb_ctx *ctx, double *ms, uint32_t *launches);
+
+/* Phase times of the last device-resident two-pass encode on this context
+ * (ms[0..3]: the set-up kernels -- prefix image, MAC tables --, the first-try
+ * pass, the retry pass, the split wide-prime MAC (0 when the MAC ran inside the
+ * PRF passes)), from events between its launches.  Returns the number of
+ * values written (at most n and 4; 0 when the last encode was not such a
+ * launch), negative on error.  Replaces nothing in the reference
+ * (instrumentation, like hb_last_kernel_ms). */
+int hb_last_kernel_phases(hb_ctx *ctx, double *ms, uint32_t n);
 
 /* Device memory helpers so that callers without a GPU framework (e.g. a cgo or
  * JNI binding) can hold a device-resident file: allocate, copy

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summary of an amd-smi sample file written by scripts/gpu_power.sh /
+"""Summary of an amd-smi sample file written by scripts/archive/gpu_power.sh /
 gpu_r4_power.sh ("== <time>" then `amd-smi metric -g 0 -p -c --json`): socket
 power and the mean gfx clock over the 8 XCDs, for the samples taken under
 load (socket power >= --min-w, default 900 W: the encode's steady state, not

@@ -50,6 +50,12 @@ def test_default_encode_line_with_every_leg(fake, monkeypatch, capsys, tmp_path)
     assert pr["workload"].startswith("configs[4]")
     assert pr["verify"]["verified"] is True
     assert d["build"]["build_id"] == "0" * 64
+    for row, bits in (("wide", 1024), ("configs1", 256)):
+        r = d[row]
+        assert r["parity_sample"]["ok"] is True and r["value"] > 0 and r["aes_per_block"] > 0, row
+        assert r["workload"].startswith("%d-bit" % bits) and set(r["phases_ms"]) and r["roofline"]["frac"] > 0
+    n = d["config"]["file_bytes_per_rank"]
+    assert d["wide"]["blocks"] == n // 1280 + 1 and d["configs1"]["blocks"] == n // 32 + 1
     hp = d["host_path"]
     assert hp["raw_tags_equal"] is True and hp["api_tags_equal"] is True
     assert hp["api_prove_file"]["equal_device_resident_proof"] is True

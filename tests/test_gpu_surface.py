@@ -27,8 +27,8 @@ P256 = int("db8709c32591ddc589b5c3c0986f92e0d11205b943c23a7e419e6c35b0256e6b", 1
 
 
 def _num_cus():
-    import torch
-    return torch.cuda.get_device_properties(0).multi_processor_count
+    from heartbeat_amd import _native
+    return _native.context().num_cus()
 
 
 def _prime(bits, seed):
@@ -99,14 +99,16 @@ def test_small_encode_alpha_at_the_position_limit(oracle, S, short):
 
 
 def test_fused_prove_after_fused_verify_small_top_limb(oracle):
-    """A 232-bit prime (top limb < 2^8): verify, then prove, then verify ...
-    on one context with the same S; every proof equals the oracle's and
-    verifies.  The prove's polled token word is cleared before its launch,
-    so the verify's mu left in the pinned results buffer cannot pass for
+    """A 249-bit prime (top limb < 2^25; 31-byte sectors, S = 16: C and the
+    32-byte tags 16-byte aligned, so the uploaded small file is proved by
+    the fused launch): prove, verify, prove ... on one context with the same
+    S; every proof equals the oracle's and verifies.  The prove's polled
+    token word (the verify's top limb of mu_{S-1} in the pinned results
+    buffer) is cleared before its launch, so a stale value cannot pass for
     the token.  Reference: PySwizzle.py:333-395."""
     from heartbeat_amd.PySwizzle import Challenge, PySwizzle
-    p = _prime(232, 232)
-    S = 4
+    p = _prime(249, 249)
+    S = 16
     data = np.random.default_rng(232).integers(0, 256, 200000, dtype=np.uint8).tobytes()
     beat = PySwizzle(S, b"k" * 32, p)
     tag, state = beat.encode(io.BytesIO(data))

@@ -77,9 +77,9 @@ def test_restored_objects_do_not_satisfy_make(tmp_path):
     """A copy of the built tree: `make -n` has nothing to do.  Then the
     stamps are made to hold another tree state's hashes (objects restored
     from a reverted experiment keep their newer mtimes, but their stamps
-    record other inputs): make wants to recompile those object groups."""
+    record other inputs): make wants to recompile those objects."""
     csrc = os.path.join(ROOT, "heartbeat_amd", "csrc")
-    if not os.path.exists(os.path.join(csrc, "build", "kern.id")):
+    if not os.path.exists(os.path.join(csrc, "build", "hb_kern_nl8.id")):
         pytest.skip("library not built with provenance stamps")
     _copy_tree(str(tmp_path), with_objects=True)
     shutil.copy2(os.path.join(ROOT, "heartbeat_amd", "libhbswizzle.so"), os.path.join(str(tmp_path), "heartbeat_amd"))
@@ -87,7 +87,7 @@ def test_restored_objects_do_not_satisfy_make(tmp_path):
     r = subprocess.run(["make", "-n", "-C", tcsrc], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert "hipcc" not in r.stdout, r.stdout
-    for stamp in ("kern.id", "rt.id"):
+    for stamp in ("hb_kern_nl8.id", "rt.id"):
         p = os.path.join(tcsrc, "build", stamp)
         with open(p, "w") as fh:
             fh.write("0" * 64 + "\n")
