@@ -25,6 +25,7 @@
 #include "../../include/hbswizzle.h"
 #include "hb_aes_host.hpp"
 #include "hb_args.hpp"
+#include "hb_wide_args.hpp"
 #include "hb_bignum_host.hpp"
 
 using namespace hbhost;
@@ -209,6 +210,7 @@ const SwitchName kSwitches[] = {
     {"HB_NO_PROVE_UPLOAD", HB_SW_NO_PROVE_UPLOAD},
     {"HB_MID_BLOCKS", HB_SW_MID_BLOCKS},
     {"HB_NO_WIDE", HB_SW_NO_WIDE},
+    {"HB_WMAC_WPE", HB_SW_WMAC_WPE},
 };
 
 int nl_for_bits(int bits) {
@@ -1158,11 +1160,13 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(hb_launch_prefix(PA, nr, c->num_cus, c->stream), "hb_prefix_kernel launch");
         c->last_launches++;
     }
-    if (wide) {
-        // the digit table and kz from alpha_j R mod p (on the device, in stream order)
-        HB_CHECK(hipMemsetAsync(WT.status, 0, 4, c->stream), "hipMemsetAsync");
-        HB_CHECK(hb_launch_wtab<NL>(WT, c->stream), "hb_wtab_kernel launch");
-        c->last_launches++;
+    if constexpr (NL >= 16) {
+        if (wide) {
+            // the digit table and kz from alpha_j R mod p (on the device, in stream order)
+            HB_CHECK(hipMemsetAsync(WT.status, 0, 4, c->stream), "hipMemsetAsync");
+            HB_CHECK(hb_launch_wtab<NL>(WT, c->stream), "hb_wtab_kernel launch");
+            c->last_launches++;
+        }
     }
     if (mf_layout) {
         // built on the host while the GPU runs the prefix kernel
@@ -1282,6 +1286,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
                 M.fsrc = A.fout;
                 M.tags = tg;
                 M.alpha_mont = (const u32 *)c->alpha_mont.p;
+                if (const char *v = sw_env(c, "HB_WMAC_WPE")) M.wpe = (u32)atoi(v);
                 HB_CHECK(hb_launch_wmac<NL>(M, c->stream), "hb_wmac_kernel launch");
                 c->last_launches += (M.nfull ? 1 : 0) + (nb > M.nfull ? 1 : 0);
             }
@@ -1479,8 +1484,14 @@ int launch_wsum(hb_ctx *c, WsumArgs<NL> &A, int align) {
     if (c->sums_in_hres) {
         if (int rc = ensure_hres(c, words)) return rc;
         A.out = c->hres;
+        // the token word finish_sums checks: a freshly grown pinned buffer
+        // (or an earlier operation) may hold any value there, this launch's
+        // token included.  Cleared before the operation's first launch only:
+        // an `accumulate` launch reads its predecessor's token from it.
+        if (!A.accumulate) c->hres[words - 1] = 0;
     } else {
         A.out = (u32 *)c->sums.p;
+        if (!A.accumulate) HB_CHECK(hipMemsetAsync(A.out + words - 1, 0, 4, c->stream), "hipMemsetAsync(token)");
     }
     A.token = next_token(c, !A.accumulate);
     HB_CHECK(hb_launch_wsum<NL>(A, align, (int)gx, c->stream), "hb_wsum_kernel launch");

@@ -5,6 +5,7 @@
 // kernels build apart from the PRF engine's translation units.
 #pragma once
 #include "hb_kernels.hpp"
+#include "hb_wide_args.hpp"
 
 // ------------------------------------------------------------------ split wide-prime MAC
 // Primes above 256 bits (hb_args.hpp, WtabArgs / WmacArgs): the PRF passes
@@ -100,30 +101,91 @@ __global__ __launch_bounds__(256) void hb_wtab_kernel(WtabArgs<NL> A) {
 }
 
 // tag = (F + sum_j alpha_j m_j) mod p for the blocks [0, nfull) of a launch
-// that lie wholly inside the data.  A wave takes 64 consecutive blocks, four
-// groups of 16 (group g: blocks 16 g .. 16 g + 15, the B columns of a
-// v_mfma_i32_16x16x64_i8); per 64-byte K slice of the blocks lane (q, n)
-// loads bytes 16 q .. 16 q + 15 of block 16 g + n for each group (the four
-// lanes n, n+16, n+32, n+48 read one contiguous 64-byte piece) and every A
-// tile of the slice is applied to the four groups.  Tile t's result at lane
+// that lie wholly inside the data.  A workgroup takes 64 consecutive blocks,
+// four groups of 16 (group g: blocks 16 g .. 16 g + 15, the B columns of a
+// v_mfma_i32_16x16x64_i8), and its HB_WMAC_WAVES waves split the Mt digit
+// tiles between them (wave v: tiles v TW .. v TW + TW - 1), so that a wave
+// holds 16 TW accumulator registers (32 at 1024 bits) instead of all 16 Mt
+// -- which at one wave per SIMD left every K slice's loads exposed (9.0 ms
+// for 8 GiB at 1024 bits, profiles/r06/b).  Per 64-byte K slice lane (q, n)
+// loads bytes 16 q .. 16 q + 15 of block 16 g + n of each group (the four
+// lanes n, n+16, n+32, n+48 read one contiguous 64-byte piece; the next
+// slice's loads go out before this slice's MFMAs), and each of the wave's A
+// tiles of the slice is applied to the four groups.  Tile t's result at lane
 // (q, n) is digits 16 t + 4 q .. + 3 of block 16 g + n, i.e. limb 4 t + q; a
 // 4 x 4 transpose of (group, lane row) -- v_permlane32_swap and
-// v_permlane16_swap -- leaves lane l with limbs 4 t .. 4 t + 3 of its own
-// block l, and the lane folds them into T = sum_c col_c 256^c + kz in limb
-// order.  At most 8 tiles are held at once (128 accumulator registers);
-// 2048-bit primes (16 tiles) take two passes over the K slices.
+// v_permlane16_swap -- leaves lane l with limbs 4 t .. 4 t + 3 of block l,
+// written to the workgroup's LDS limb table ([limb][block]: conflict-free).
+// Wave 0 then folds each block's limbs into T = sum_c col_c 256^c + kz in
+// limb order (one lane per block), adds F and reduces.
+#ifndef HB_WMAC_WAVES
+#define HB_WMAC_WAVES 4
+#endif
+// v (NL+1 limbs, v < 2^32 p) -> v mod p in place (limbs 0..NL-1), as
+// hb_reduce_small but without its second NL+1-limb array: the comparison
+// with p runs first and the subtraction in place (registers of the MAC
+// kernel's finish, which set its occupancy)
 template <int NL>
-struct HbWmac {
-    static constexpr int MTP = NL / 4 < 8 ? NL / 4 : 8;   // tiles per pass
-    static constexpr int NP = (NL / 4 + MTP - 1) / MTP;    // passes for D = 4 NL
-};
+__device__ __forceinline__ void hb_reduce_small_lean(u32 v[NL + 1], const ModP<NL> &P) {
+    constexpr int T0 = NL - 2 - 31 > 0 ? NL - 2 - 31 : 0;
+    double vd = 0.0, sc = HbScale<NL, T0>::v;
+    HB_UNROLL
+    for (int t = T0; t <= NL; ++t) {
+        vd += (double)v[t] * sc;
+        sc *= 4294967296.0;
+    }
+    const double qd = vd * P.inv_scaled;
+    const u32 q = qd >= 2.0 ? (u32)qd - 1u : 0u;   // floor(qd) - 1 <= true quotient
+    u64 carry = 0;
+    u32 borrow = 0;
+    HB_UNROLL
+    for (int t = 0; t <= NL; ++t) {
+        const u64 pr = (u64)q * (t < NL ? P.p[t] : 0u) + carry;
+        carry = pr >> 32;
+        const u64 d = (u64)v[t] - (u32)pr - borrow;
+        v[t] = (u32)d;
+        borrow = (u32)(d >> 63);
+    }
+    for (;;) {   // at most a few iterations: v >= p ?
+        bool ge = v[NL] != 0, decided = ge;
+        HB_UNROLL
+        for (int t = NL - 1; t >= 0; --t) {
+            const bool d = !decided && v[t] != P.p[t];
+            ge = d ? v[t] > P.p[t] : ge;
+            decided = decided || d;
+        }
+        if (decided && !ge) break;   // v < p; otherwise v >= p (all limbs equal: v == p)
+        u32 br = 0;
+        HB_UNROLL
+        for (int t = 0; t <= NL; ++t) {
+            const u64 d = (u64)v[t] - (t < NL ? P.p[t] : 0u) - br;
+            v[t] = (u32)d;
+            br = (u32)(d >> 63);
+        }
+    }
+}
 
 template <int NL>
-__global__ __launch_bounds__(256) void hb_wmac_kernel(WmacArgs<NL> A) {
-    constexpr int MTP = HbWmac<NL>::MTP, NP = HbWmac<NL>::NP;
-    const u32 l = hb_lane_id(), q = l >> 4, n = l & 15u;
-    const u64 w0 = ((u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64u;
-    if (w0 >= A.nfull) return;   // wave-uniform
+struct HbWmac {
+    static constexpr int TW = (NL / 4 + HB_WMAC_WAVES - 1) / HB_WMAC_WAVES;   // tiles per wave (D <= 4 NL)
+};
+
+// WPE: waves per SIMD the register allocator is held to (occupancy of the
+// load-latency-bound K loop); 0 = the compiler's choice.  The launcher takes
+// HB_WMAC_WPE unless WmacArgs::wpe (test switch $HB_WMAC_WPE, A/B) names
+// another instantiated value.
+#ifndef HB_WMAC_WPE
+#define HB_WMAC_WPE 4
+#endif
+template <int WPE>
+struct HbWpe { static constexpr int v = WPE > 0 ? WPE : 1; };
+template <int NL, int WPE>
+__global__ __launch_bounds__(64 * HB_WMAC_WAVES) __attribute__((amdgpu_waves_per_eu(HbWpe<WPE>::v)))
+void hb_wmac_kernel(WmacArgs<NL> A) {
+    constexpr int TW = HbWmac<NL>::TW;
+    __shared__ long long lim[NL * 64];   // [limb][block] signed limb sums of the 64 blocks
+    const u32 l = hb_lane_id(), q = l >> 4, n = l & 15u, wv = threadIdx.x >> 6;
+    const u64 w0 = (u64)blockIdx.x * 64u;
     const unsigned char *bp[4];
     bool okg[4];
 #pragma unroll
@@ -132,103 +194,97 @@ __global__ __launch_bounds__(256) void hb_wmac_kernel(WmacArgs<NL> A) {
         okg[g] = b < A.nfull;
         bp[g] = A.data + (okg[g] ? b : w0) * A.C + 16u * q;
     }
-    const hb_i32x4 *afr = reinterpret_cast<const hb_i32x4 *>(A.afrag);
-    u32 T[NL + 1];
-    long long carry = 0;
+    const u32 t0 = wv * (u32)TW;
+    if (t0 < A.Mt) {   // wave-uniform
+        hb_i32x4 acc[TW][4];
 #pragma unroll
-    for (int P = 0; P < NP; ++P) {
-        const u32 t0 = (u32)(P * MTP);
-        if (t0 < A.Mt) {   // uniform
-            hb_i32x4 acc[MTP][4];
+        for (int t = 0; t < TW; ++t)
 #pragma unroll
-            for (int t = 0; t < MTP; ++t)
+            for (int g = 0; g < 4; ++g) acc[t][g] = hb_i32x4{0, 0, 0, 0};
+        auto load = [&](u32 s, hb_i32x4 dst[4]) {
+            const bool in = 64u * s + 16u * q < A.C;   // 16-byte pieces past the block: zero
 #pragma unroll
-                for (int g = 0; g < 4; ++g) acc[t][g] = hb_i32x4{0, 0, 0, 0};
-            for (u32 s = 0; s < A.nslices; ++s) {
-                const bool in = 64u * s + 16u * q < A.C;   // 16-byte pieces past the block: zero
-                hb_i32x4 b[4];
+            for (int g = 0; g < 4; ++g)
+                dst[g] = okg[g] && in ? *reinterpret_cast<const hb_i32x4 *>(bp[g] + 64u * s) : hb_i32x4{0, 0, 0, 0};
+        };
+        const hb_i32x4 *afr = reinterpret_cast<const hb_i32x4 *>(A.afrag) + (u64)t0 * 64u + l;
+        hb_i32x4 b[4], bn[4];
+        load(0, b);
+        for (u32 s = 0; s < A.nslices; ++s) {
+            if (s + 1 < A.nslices) load(s + 1, bn);
+            hb_i32x4 a[TW];
+#pragma unroll
+            for (int t = 0; t < TW; ++t)
+                a[t] = t0 + (u32)t < A.Mt ? afr[((u64)s * A.Mt + (u32)t) * 64u] : hb_i32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int g = 0; g < 4; ++g) b[g] ^= (int32_t)0x80808080;
+#pragma unroll
+            for (int t = 0; t < TW; ++t)
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
-                    b[g] = okg[g] && in ? *reinterpret_cast<const hb_i32x4 *>(bp[g] + 64u * s) : hb_i32x4{0, 0, 0, 0};
+                    acc[t][g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t], b[g], acc[t][g], 0, 0, 0);
 #pragma unroll
-                for (int g = 0; g < 4; ++g) b[g] ^= (int32_t)0x80808080;
-                const hb_i32x4 *as = afr + ((u64)s * A.Mt + t0) * 64u + l;
+            for (int g = 0; g < 4; ++g) b[g] = bn[g];
+        }
 #pragma unroll
-                for (int t = 0; t < MTP; ++t) {
-                    if (t0 + (u32)t < A.Mt) {
-                        const hb_i32x4 a = as[(u64)t * 64u];
+        for (int t = 0; t < TW; ++t) {
+            if (t0 + (u32)t < A.Mt) {
+                u32 X[4][2];
 #pragma unroll
-                        for (int g = 0; g < 4; ++g)
-                            acc[t][g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b[g], acc[t][g], 0, 0, 0);
-                    }
+                for (int g = 0; g < 4; ++g) {
+                    const hb_i32x4 &a = acc[t][g];
+                    const long long v = (long long)a[0] + ((long long)a[1] << 8) + ((long long)a[2] << 16) +
+                                        ((long long)a[3] << 24);
+                    X[g][0] = (u32)v;
+                    X[g][1] = (u32)((u64)v >> 32);
                 }
-            }
 #pragma unroll
-            for (int t = 0; t < MTP; ++t) {
-                if (t0 + (u32)t < A.Mt) {
-                    u32 X[4][2];
+                for (int d = 0; d < 2; ++d) {
+                    const auto s02 = __builtin_amdgcn_permlane32_swap((int)X[0][d], (int)X[2][d], false, false);
+                    const auto s13 = __builtin_amdgcn_permlane32_swap((int)X[1][d], (int)X[3][d], false, false);
+                    const auto s01 = __builtin_amdgcn_permlane16_swap((int)s02[0], (int)s13[0], false, false);
+                    const auto s23 = __builtin_amdgcn_permlane16_swap((int)s02[1], (int)s13[1], false, false);
+                    X[0][d] = (u32)s01[0];
+                    X[1][d] = (u32)s01[1];
+                    X[2][d] = (u32)s23[0];
+                    X[3][d] = (u32)s23[1];
+                }
+                // X[s]: limb 4 (t0 + t) + s of block l
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const hb_i32x4 &a = acc[t][g];
-                        const long long v = (long long)a[0] + ((long long)a[1] << 8) + ((long long)a[2] << 16) +
-                                            ((long long)a[3] << 24);
-                        X[g][0] = (u32)v;
-                        X[g][1] = (u32)((u64)v >> 32);
-                    }
-#pragma unroll
-                    for (int d = 0; d < 2; ++d) {
-                        const auto s02 = __builtin_amdgcn_permlane32_swap((int)X[0][d], (int)X[2][d], false, false);
-                        const auto s13 = __builtin_amdgcn_permlane32_swap((int)X[1][d], (int)X[3][d], false, false);
-                        const auto s01 = __builtin_amdgcn_permlane16_swap((int)s02[0], (int)s13[0], false, false);
-                        const auto s23 = __builtin_amdgcn_permlane16_swap((int)s02[1], (int)s13[1], false, false);
-                        X[0][d] = (u32)s01[0];
-                        X[1][d] = (u32)s01[1];
-                        X[2][d] = (u32)s23[0];
-                        X[3][d] = (u32)s23[1];
-                    }
-                    // X[s]: limb 4 (t0 + t) + s of this lane's block
-#pragma unroll
-                    for (int s4 = 0; s4 < 4; ++s4) {
-                        const int i = 4 * (P * MTP + t) + s4;
-                        if (i < NL) {
-                            const long long L = (long long)(((u64)X[s4][1] << 32) | X[s4][0]);
-                            const long long xv = (long long)A.kz[i] + L + carry;
-                            T[i] = (u32)xv;
-                            carry = xv >> 32;
-                        }
-                    }
+                for (int s4 = 0; s4 < 4; ++s4) {
+                    const u32 i = 4u * (t0 + (u32)t) + (u32)s4;
+                    if (i < (u32)NL) lim[i * 64u + l] = (long long)(((u64)X[s4][1] << 32) | X[s4][0]);
                 }
             }
         }
     }
-    // limbs above the tiles' digits: kz and the carry only
-#pragma unroll
-    for (int i = 0; i <= NL; ++i) {
-        if ((u32)i >= 4u * A.Mt) {
-            const long long xv = (long long)A.kz[i] + carry;
-            T[i] = (u32)xv;
-            carry = xv >> 32;
-        }
-    }
+    __syncthreads();
+    if (wv != 0) return;
     const u64 blk = w0 + l;
     if (blk >= A.nfull) return;
-    u32 F[NL], v[NL + 1], tag[NL];
+    // v = T + F, T = sum_i lim_i 2^(32 i) + kz (limbs past the tiles' digits: kz and the carry)
+    const u32 lt = 4u * A.Mt;
     const u32 *fp = A.fsrc + blk * NL;
+    u32 v[NL + 1];
+    long long carry = 0;
+    u64 c = 0;
 #pragma unroll
     for (int t = 0; t < NL; t += 4) {
         const uint4 f = *reinterpret_cast<const uint4 *>(fp + t);
-        F[t] = f.x; F[t + 1] = f.y; F[t + 2] = f.z; F[t + 3] = f.w;
-    }
-    u64 c = 0;
+        const u32 F4[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-    for (int t = 0; t < NL; ++t) {
-        c += (u64)T[t] + F[t];
-        v[t] = (u32)c;
-        c >>= 32;
+        for (int k = 0; k < 4; ++k) {
+            const u32 i = (u32)(t + k);
+            const long long xv = (long long)A.kz[i] + (i < lt ? lim[i * 64u + l] : 0ll) + carry;
+            carry = xv >> 32;
+            c += (u64)(u32)xv + F4[k];
+            v[t + k] = (u32)c;
+            c >>= 32;
+        }
     }
-    v[NL] = T[NL] + (u32)c;
-    hb_reduce_small<NL>(v, A.mod, tag);
-    hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, tag);
+    v[NL] = (u32)((long long)A.kz[NL] + carry) + (u32)c;
+    hb_reduce_small_lean<NL>(v, A.mod);
+    hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, v);
 }
 
 // The blocks [nfull, nblocks) of a split encode (the short last block and any
@@ -254,13 +310,16 @@ hipError_t hb_launch_wtab(const WtabArgs<NL> &A, hipStream_t s) {
 template <int NL>
 hipError_t hb_launch_wmac(const WmacArgs<NL> &A, hipStream_t s) {
     if (hb_load_only) {
-        hb_load_kernel(&hb_wmac_kernel<NL>);
+        hb_load_kernel(&hb_wmac_kernel<NL, (NL >= 64 ? 0 : HB_WMAC_WPE)>);
         hb_load_kernel(&hb_wmac_tail_kernel<NL>);
         return hipSuccess;
     }
     if (A.nfull) {
-        const u64 waves = (A.nfull + 63) / 64;
-        HB_LAUNCH((hb_wmac_kernel<NL>), dim3((u32)((waves + 3) / 4)), dim3(256), s, A);
+        const dim3 g((u32)((A.nfull + 63) / 64)), b(64 * HB_WMAC_WAVES);
+        if (A.wpe == 3) HB_LAUNCH((hb_wmac_kernel<NL, 3>), g, b, s, A);
+        else if (A.wpe == 5) HB_LAUNCH((hb_wmac_kernel<NL, 5>), g, b, s, A);
+        else if (A.wpe == 1) HB_LAUNCH((hb_wmac_kernel<NL, 0>), g, b, s, A);
+        else HB_LAUNCH((hb_wmac_kernel<NL, (NL >= 64 ? 0 : HB_WMAC_WPE)>), g, b, s, A);
     }
     if (A.nblocks > A.nfull) {
         const u64 n = A.nblocks - A.nfull;

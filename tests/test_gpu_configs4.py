@@ -138,6 +138,22 @@ def test_configs1_host_gather_prove_at_26_bit_index_width(oracle):
         tags = np.empty(nb * w, dtype=np.uint8)
         ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data, dptr.value, length, 2))
         ctx.check(L.hb_memcpy(ctx.h, tags.ctypes.data, tptr.value, nb * w, 2))
+        # the full-size configs[1] tags themselves against the oracle: the
+        # first and last 1,000 blocks (the PRF-only tail block included) and
+        # 10,000 random ones (PySwizzle.py:296-309 at S = 1)
+        rng = np.random.default_rng(0xC1)
+        picks = sorted(set(range(1000)) | set(range(nb - 1000, nb)) | set(rng.integers(0, nb, 10000).tolist()))
+        runs, i = [], 0
+        while i < len(picks):
+            j = i
+            while j + 1 < len(picks) and picks[j + 1] == picks[j] + 1:
+                j += 1
+            runs.append((picks[i], picks[j] + 1))
+            i = j + 1
+        for r0, r1 in runs:
+            want = oracle.encode(p, S, b"f" * 32, b"a" * 32, host[r0 * C:r1 * C].tobytes(), block_base=r0,
+                                 nblocks=r1 - r0, nthreads=4)
+            assert tags[r0 * w:r1 * w].tobytes() == b"".join(t.to_bytes(w, "big") for t in want), (r0, r1)
         res = []
         for tp, dp, flags in ((tptr.value, dptr.value, 3), (tags.ctypes.data, host.ctypes.data, 0)):
             mu = ctypes.create_string_buffer(w * S)
