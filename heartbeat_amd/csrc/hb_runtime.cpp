@@ -1273,7 +1273,6 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
                 M.mod = A.mod;
                 M.data = d;
                 M.len = dlen;
-                M.nblocks = nb;
                 M.nfull = dlen / C < nb ? dlen / C : nb;
                 M.C = C;
                 M.ss = pi.ss;
@@ -1285,10 +1284,22 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
                 M.kz = WT.kz;
                 M.fsrc = A.fout;
                 M.tags = tg;
-                M.alpha_mont = (const u32 *)c->alpha_mont.p;
                 if (const char *v = sw_env(c, "HB_WMAC_WPE")) M.wpe = (u32)atoi(v);
                 HB_CHECK(hb_launch_wmac<NL>(M, c->stream), "hb_wmac_kernel launch");
-                c->last_launches += (M.nfull ? 1 : 0) + (nb > M.nfull ? 1 : 0);
+                c->last_launches += M.nfull ? 1 : 0;
+                if (nb > M.nfull) {
+                    // the short last block (and any past the end of the data):
+                    // the small path's MAC kernel, the block's sectors over lanes
+                    EncodeArgs<NL> T = A;
+                    T.data = d + M.nfull * C;
+                    T.len = dlen - M.nfull * C;
+                    T.nblocks = nb - M.nfull;
+                    T.tags = tg + M.nfull * pi.tw;
+                    T.fv = A.fout + M.nfull * NL;
+                    HB_CHECK(hb_launch_mac<NL>(T, full16(pi, NL, C, T.data) ? 16 : 1, c->stream),
+                             "hb_mac_kernel launch");
+                    c->last_launches++;
+                }
             }
         }
         return 0;

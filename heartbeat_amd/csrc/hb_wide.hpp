@@ -1,7 +1,7 @@
 // hb_wide.hpp -- the split wide-prime encode's MAC kernels (primes above 256
 // bits): the device-built int8 digit table (hb_wtab_kernel) and the MFMA MAC
-// that turns the PRF passes' F into tags (hb_wmac_kernel, the VALU tail
-// hb_wmac_tail_kernel).  Instantiated by hb_kern_wide.hip only, so that these
+// that turns the PRF passes' F into tags (hb_wmac_kernel; the short last
+// block goes through hb_mac_split_kernel / hb_mac_kernel, hb_runtime.cpp).  Instantiated by hb_kern_wide.hip only, so that these
 // kernels build apart from the PRF engine's translation units.
 #pragma once
 #include "hb_kernels.hpp"
@@ -100,27 +100,6 @@ __global__ __launch_bounds__(256) void hb_wtab_kernel(WtabArgs<NL> A) {
     if (carry != (neg ? 1u : 0u)) atomicOr(A.status, 1u);
 }
 
-// tag = (F + sum_j alpha_j m_j) mod p for the blocks [0, nfull) of a launch
-// that lie wholly inside the data.  A workgroup takes 64 consecutive blocks,
-// four groups of 16 (group g: blocks 16 g .. 16 g + 15, the B columns of a
-// v_mfma_i32_16x16x64_i8), and its HB_WMAC_WAVES waves split the Mt digit
-// tiles between them (wave v: tiles v TW .. v TW + TW - 1), so that a wave
-// holds 16 TW accumulator registers (32 at 1024 bits) instead of all 16 Mt
-// -- which at one wave per SIMD left every K slice's loads exposed (9.0 ms
-// for 8 GiB at 1024 bits, profiles/r06/b).  Per 64-byte K slice lane (q, n)
-// loads bytes 16 q .. 16 q + 15 of block 16 g + n of each group (the four
-// lanes n, n+16, n+32, n+48 read one contiguous 64-byte piece; the next
-// slice's loads go out before this slice's MFMAs), and each of the wave's A
-// tiles of the slice is applied to the four groups.  Tile t's result at lane
-// (q, n) is digits 16 t + 4 q .. + 3 of block 16 g + n, i.e. limb 4 t + q; a
-// 4 x 4 transpose of (group, lane row) -- v_permlane32_swap and
-// v_permlane16_swap -- leaves lane l with limbs 4 t .. 4 t + 3 of block l,
-// written to the workgroup's LDS limb table ([limb][block]: conflict-free).
-// Wave 0 then folds each block's limbs into T = sum_c col_c 256^c + kz in
-// limb order (one lane per block), adds F and reduces.
-#ifndef HB_WMAC_WAVES
-#define HB_WMAC_WAVES 4
-#endif
 // v (NL+1 limbs, v < 2^32 p) -> v mod p in place (limbs 0..NL-1), as
 // hb_reduce_small but without its second NL+1-limb array: the comparison
 // with p runs first and the subtraction in place (registers of the MAC
@@ -165,102 +144,186 @@ __device__ __forceinline__ void hb_reduce_small_lean(u32 v[NL + 1], const ModP<N
     }
 }
 
+// tag = (F + sum_j alpha_j m_j) mod p for the blocks [0, nfull) of a launch
+// that lie wholly inside the data.  A workgroup of HB_WMAC_WAVES waves takes
+// 16 NG consecutive blocks, NG groups of 16 (group g: the B columns of a
+// v_mfma_i32_16x16x64_i8), and its waves split the Mt digit tiles (wave v:
+// tiles v TW .. v TW + TW - 1), so a wave holds 16 NG TW accumulator
+// registers.  The blocks' bytes go through LDS once per workgroup, one 64-byte
+// K slice of every block at a time, double-buffered: the workgroup's threads
+// load slice s + 1 (four threads per 64-byte piece, coalesced) while the waves
+// run slice s's MFMAs from LDS; each A fragment (global, L2-resident) serves
+// the NG groups.  Every 16-byte piece is read from HBM once and every A
+// fragment once per 16 NG blocks per wave (with the blocks read by every wave
+// straight from global memory and 4 groups, the kernel took 5.7 ms for 8 GiB
+// at 1024 bits, profiles/r06/c; with one wave holding all Mt tiles, 9.0 ms
+// at one wave per SIMD, profiles/r06/b).  Tile t's result at lane (q, n) is
+// digits 16 t + 4 q .. + 3 of block 16 g + n, i.e. limb 4 t + q; a 4 x 4
+// transpose of (group within a quad of groups, lane row) --
+// v_permlane32_swap, v_permlane16_swap -- leaves lane l with limbs 4 t ..
+// 4 t + 3 of block 64 h + l of group quad h, written to the LDS limb table
+// ([limb][block]: conflict-free), which reuses the slice buffers.  One lane
+// per block then folds the limbs into T = sum_c col_c 256^c + kz in limb
+// order, adds F and reduces.
+#ifndef HB_WMAC_WAVES
+#define HB_WMAC_WAVES 4
+#endif
+// K slices in flight from global memory per thread (registers)
+#ifndef HB_WMAC_PF
+#define HB_WMAC_PF 3
+#endif
+#ifndef HB_WMAC_NG
+#define HB_WMAC_NG 8
+#endif
 template <int NL>
 struct HbWmac {
-    static constexpr int TW = (NL / 4 + HB_WMAC_WAVES - 1) / HB_WMAC_WAVES;   // tiles per wave (D <= 4 NL)
+    static constexpr int NG = NL >= 64 ? HB_WMAC_WAVES : HB_WMAC_NG;            // groups of 16 blocks
+    static constexpr int NB = 16 * NG;                                          // blocks per workgroup
+    static constexpr int TW = (NL / 4 + HB_WMAC_WAVES - 1) / HB_WMAC_WAVES;    // tiles per wave (D <= 4 NL)
+    // LDS: two slice buffers (NB x 64 bytes each), or the limb table (NL x NB x 8 bytes)
+    static constexpr int LDS_BYTES = 2 * NB * 64 > NL * NB * 8 ? 2 * NB * 64 : NL * NB * 8;
 };
 
-// WPE: waves per SIMD the register allocator is held to (occupancy of the
-// load-latency-bound K loop); 0 = the compiler's choice.  The launcher takes
-// HB_WMAC_WPE unless WmacArgs::wpe (test switch $HB_WMAC_WPE, A/B) names
-// another instantiated value.
+// WPE: waves per SIMD the register allocator is held to; 0 = the compiler's
+// choice.  The launcher takes HB_WMAC_WPE unless WmacArgs::wpe (test switch
+// $HB_WMAC_WPE, A/B) names another instantiated value.
 #ifndef HB_WMAC_WPE
-#define HB_WMAC_WPE 4
+#define HB_WMAC_WPE 3
 #endif
 template <int WPE>
 struct HbWpe { static constexpr int v = WPE > 0 ? WPE : 1; };
 template <int NL, int WPE>
 __global__ __launch_bounds__(64 * HB_WMAC_WAVES) __attribute__((amdgpu_waves_per_eu(HbWpe<WPE>::v)))
 void hb_wmac_kernel(WmacArgs<NL> A) {
-    constexpr int TW = HbWmac<NL>::TW;
-    __shared__ long long lim[NL * 64];   // [limb][block] signed limb sums of the 64 blocks
-    const u32 l = hb_lane_id(), q = l >> 4, n = l & 15u, wv = threadIdx.x >> 6;
-    const u64 w0 = (u64)blockIdx.x * 64u;
-    const unsigned char *bp[4];
-    bool okg[4];
+    constexpr int NG = HbWmac<NL>::NG, NB = HbWmac<NL>::NB, TW = HbWmac<NL>::TW;
+    constexpr int NT = 64 * HB_WMAC_WAVES;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[HbWmac<NL>::LDS_BYTES];
+    const u32 l = hb_lane_id(), wv = threadIdx.x >> 6;
+    const u64 w0 = (u64)blockIdx.x * NB;
+    // slice loads: piece u = r NT + threadIdx.x, r < NB 4 / NT: block u / 4,
+    // bytes 16 (u % 4) .. + 15 of the slice; stored at LDS unit (g, u % 4, n)
+    // of its group g = (u / 4) / 16, n = (u / 4) % 16 -- lane (q, n) of a wave
+    // reads unit (g, q, n): consecutive lanes, consecutive 16 bytes
+    constexpr int LR = NB * 4 / NT;   // 16-byte pieces per thread per slice
+    const unsigned char *src[LR];
+    bool okp[LR];
+    u32 dst[LR];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const u64 b = w0 + 16u * (u32)g + n;
-        okg[g] = b < A.nfull;
-        bp[g] = A.data + (okg[g] ? b : w0) * A.C + 16u * q;
+    for (int r = 0; r < LR; ++r) {
+        const u32 u = (u32)r * NT + threadIdx.x, b = u >> 2, qq = u & 3u;
+        const u64 blk = w0 + b;
+        okp[r] = blk < A.nfull;
+        src[r] = A.data + (okp[r] ? blk : w0) * A.C + 16u * qq;
+        dst[r] = (((b >> 4) * 4u + qq) * 16u + (b & 15u)) * 16u;
     }
+    auto gload = [&](u32 s, hb_i32x4 v[LR]) {
+#pragma unroll
+        for (int r = 0; r < LR; ++r) {
+            const bool in = okp[r] && 64u * s + 16u * ((threadIdx.x + (u32)r * NT) & 3u) < A.C;
+            v[r] = in ? *reinterpret_cast<const hb_i32x4 *>(src[r] + 64u * s) : hb_i32x4{0, 0, 0, 0};
+        }
+    };
+    auto lstore = [&](u32 buf, const hb_i32x4 v[LR]) {
+#pragma unroll
+        for (int r = 0; r < LR; ++r)
+            *reinterpret_cast<hb_i32x4 *>(lds + buf * (NB * 64) + dst[r]) = v[r] ^ (int32_t)0x80808080;
+    };
     const u32 t0 = wv * (u32)TW;
-    if (t0 < A.Mt) {   // wave-uniform
-        hb_i32x4 acc[TW][4];
+    const bool mine = t0 < A.Mt;   // wave-uniform: this wave has tiles
+    hb_i32x4 acc[TW][NG];
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) acc[t][g] = hb_i32x4{0, 0, 0, 0};
+    const hb_i32x4 *afr = reinterpret_cast<const hb_i32x4 *>(A.afrag) + (u64)t0 * 64u + l;
+    // slices go global -> registers HB_WMAC_PF slices ahead (slot x % PF
+    // holds slice x), registers -> LDS one slice ahead (double buffer)
+    constexpr int PF = HB_WMAC_PF;
+    hb_i32x4 pv[PF][LR];
+#pragma unroll
+    for (int k = 0; k < PF; ++k)
+        if ((u32)k < A.nslices) gload((u32)k, pv[k]);
+    lstore(0, pv[0]);
+    if ((u32)PF < A.nslices) gload((u32)PF, pv[0]);
+    __syncthreads();
+    // this wave's A fragments of the slice, one slice ahead
+    auto aload = [&](u32 s, hb_i32x4 a[TW]) {
 #pragma unroll
         for (int t = 0; t < TW; ++t)
+            a[t] = mine && t0 + (u32)t < A.Mt ? afr[((u64)s * A.Mt + (u32)t) * 64u] : hb_i32x4{0, 0, 0, 0};
+    };
+    hb_i32x4 an[TW];
+    aload(0, an);
+    for (u32 s0 = 0; s0 < A.nslices; s0 += PF) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) acc[t][g] = hb_i32x4{0, 0, 0, 0};
-        auto load = [&](u32 s, hb_i32x4 dst[4]) {
-            const bool in = 64u * s + 16u * q < A.C;   // 16-byte pieces past the block: zero
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                dst[g] = okg[g] && in ? *reinterpret_cast<const hb_i32x4 *>(bp[g] + 64u * s) : hb_i32x4{0, 0, 0, 0};
-        };
-        const hb_i32x4 *afr = reinterpret_cast<const hb_i32x4 *>(A.afrag) + (u64)t0 * 64u + l;
-        hb_i32x4 b[4], bn[4];
-        load(0, b);
-        for (u32 s = 0; s < A.nslices; ++s) {
-            if (s + 1 < A.nslices) load(s + 1, bn);
+        for (int k = 0; k < PF; ++k) {
+            const u32 s = s0 + (u32)k;
+            if (s >= A.nslices) break;   // uniform
+            const u32 cur = s & 1u;
             hb_i32x4 a[TW];
 #pragma unroll
-            for (int t = 0; t < TW; ++t)
-                a[t] = t0 + (u32)t < A.Mt ? afr[((u64)s * A.Mt + (u32)t) * 64u] : hb_i32x4{0, 0, 0, 0};
+            for (int t = 0; t < TW; ++t) a[t] = an[t];
+            if (s + 1 < A.nslices) aload(s + 1, an);
+            if (mine) {
+                const unsigned char *bb = lds + cur * (NB * 64) + l * 16u;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) b[g] ^= (int32_t)0x80808080;
+                for (int g = 0; g < NG; ++g) {
+                    const hb_i32x4 b = *reinterpret_cast<const hb_i32x4 *>(bb + (u32)g * 1024u);
 #pragma unroll
-            for (int t = 0; t < TW; ++t)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    acc[t][g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t], b[g], acc[t][g], 0, 0, 0);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) b[g] = bn[g];
+                    for (int t = 0; t < TW; ++t)
+                        acc[t][g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[t], b, acc[t][g], 0, 0, 0);
+                }
+            }
+            const int nx = (k + 1) % PF;   // the slot of slice s + 1 (static once unrolled)
+            if (s + 1 < A.nslices) {
+                lstore(cur ^ 1u, pv[nx]);
+                if (s + 1 + PF < A.nslices) gload(s + 1 + PF, pv[nx]);
+            }
+            __syncthreads();
         }
+    }
+    // the slice buffers are free (every wave passed the last barrier): limb table
+    long long *lim = reinterpret_cast<long long *>(lds);
+    if (mine) {
 #pragma unroll
         for (int t = 0; t < TW; ++t) {
             if (t0 + (u32)t < A.Mt) {
-                u32 X[4][2];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const hb_i32x4 &a = acc[t][g];
-                    const long long v = (long long)a[0] + ((long long)a[1] << 8) + ((long long)a[2] << 16) +
-                                        ((long long)a[3] << 24);
-                    X[g][0] = (u32)v;
-                    X[g][1] = (u32)((u64)v >> 32);
-                }
+                for (int h = 0; h < NG / 4; ++h) {
+                    u32 X[4][2];
 #pragma unroll
-                for (int d = 0; d < 2; ++d) {
-                    const auto s02 = __builtin_amdgcn_permlane32_swap((int)X[0][d], (int)X[2][d], false, false);
-                    const auto s13 = __builtin_amdgcn_permlane32_swap((int)X[1][d], (int)X[3][d], false, false);
-                    const auto s01 = __builtin_amdgcn_permlane16_swap((int)s02[0], (int)s13[0], false, false);
-                    const auto s23 = __builtin_amdgcn_permlane16_swap((int)s02[1], (int)s13[1], false, false);
-                    X[0][d] = (u32)s01[0];
-                    X[1][d] = (u32)s01[1];
-                    X[2][d] = (u32)s23[0];
-                    X[3][d] = (u32)s23[1];
-                }
-                // X[s]: limb 4 (t0 + t) + s of block l
+                    for (int g = 0; g < 4; ++g) {
+                        const hb_i32x4 &a = acc[t][4 * h + g];
+                        const long long v = (long long)a[0] + ((long long)a[1] << 8) + ((long long)a[2] << 16) +
+                                            ((long long)a[3] << 24);
+                        X[g][0] = (u32)v;
+                        X[g][1] = (u32)((u64)v >> 32);
+                    }
 #pragma unroll
-                for (int s4 = 0; s4 < 4; ++s4) {
-                    const u32 i = 4u * (t0 + (u32)t) + (u32)s4;
-                    if (i < (u32)NL) lim[i * 64u + l] = (long long)(((u64)X[s4][1] << 32) | X[s4][0]);
+                    for (int d = 0; d < 2; ++d) {
+                        const auto s02 = __builtin_amdgcn_permlane32_swap((int)X[0][d], (int)X[2][d], false, false);
+                        const auto s13 = __builtin_amdgcn_permlane32_swap((int)X[1][d], (int)X[3][d], false, false);
+                        const auto s01 = __builtin_amdgcn_permlane16_swap((int)s02[0], (int)s13[0], false, false);
+                        const auto s23 = __builtin_amdgcn_permlane16_swap((int)s02[1], (int)s13[1], false, false);
+                        X[0][d] = (u32)s01[0];
+                        X[1][d] = (u32)s01[1];
+                        X[2][d] = (u32)s23[0];
+                        X[3][d] = (u32)s23[1];
+                    }
+                    // X[s]: limb 4 (t0 + t) + s of block 64 h + l
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; ++s4) {
+                        const u32 i = 4u * (t0 + (u32)t) + (u32)s4;
+                        if (i < (u32)NL) lim[i * NB + 64u * h + l] = (long long)(((u64)X[s4][1] << 32) | X[s4][0]);
+                    }
                 }
             }
         }
     }
     __syncthreads();
-    if (wv != 0) return;
-    const u64 blk = w0 + l;
+    if (threadIdx.x >= NB) return;
+    const u32 bi = threadIdx.x;   // block of this lane
+    const u64 blk = w0 + bi;
     if (blk >= A.nfull) return;
     // v = T + F, T = sum_i lim_i 2^(32 i) + kz (limbs past the tiles' digits: kz and the carry)
     const u32 lt = 4u * A.Mt;
@@ -275,7 +338,7 @@ void hb_wmac_kernel(WmacArgs<NL> A) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const u32 i = (u32)(t + k);
-            const long long xv = (long long)A.kz[i] + (i < lt ? lim[i * 64u + l] : 0ll) + carry;
+            const long long xv = (long long)A.kz[i] + (i < lt ? lim[i * NB + bi] : 0ll) + carry;
             carry = xv >> 32;
             c += (u64)(u32)xv + F4[k];
             v[t + k] = (u32)c;
@@ -285,18 +348,6 @@ void hb_wmac_kernel(WmacArgs<NL> A) {
     v[NL] = (u32)((long long)A.kz[NL] + carry) + (u32)c;
     hb_reduce_small_lean<NL>(v, A.mod);
     hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, v);
-}
-
-// The blocks [nfull, nblocks) of a split encode (the short last block and any
-// past the end of the data): one lane each, the VALU MAC (hb_block_tag).
-template <int NL>
-__global__ __launch_bounds__(64) void hb_wmac_tail_kernel(WmacArgs<NL> A) {
-    const u64 blk = A.nfull + (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blk >= A.nblocks) return;
-    u32 F[NL], tag[NL];
-    for (int t = 0; t < NL; ++t) F[t] = A.fsrc[blk * NL + t];
-    hb_block_tag<NL, 1>(A.data, A.len, blk, A.C, A.ss, A.S, A.alpha_mont, A.mod, F, tag);
-    hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, tag);
 }
 
 // ------------------------------------------------------------------ launchers
@@ -310,20 +361,16 @@ hipError_t hb_launch_wtab(const WtabArgs<NL> &A, hipStream_t s) {
 template <int NL>
 hipError_t hb_launch_wmac(const WmacArgs<NL> &A, hipStream_t s) {
     if (hb_load_only) {
-        hb_load_kernel(&hb_wmac_kernel<NL, (NL >= 64 ? 0 : HB_WMAC_WPE)>);
-        hb_load_kernel(&hb_wmac_tail_kernel<NL>);
+        hb_load_kernel(&hb_wmac_kernel<NL, HB_WMAC_WPE>);
         return hipSuccess;
     }
     if (A.nfull) {
-        const dim3 g((u32)((A.nfull + 63) / 64)), b(64 * HB_WMAC_WAVES);
+        const dim3 g((u32)((A.nfull + HbWmac<NL>::NB - 1) / HbWmac<NL>::NB)), b(64 * HB_WMAC_WAVES);
         if (A.wpe == 3) HB_LAUNCH((hb_wmac_kernel<NL, 3>), g, b, s, A);
+        else if (A.wpe == 4) HB_LAUNCH((hb_wmac_kernel<NL, 4>), g, b, s, A);
         else if (A.wpe == 5) HB_LAUNCH((hb_wmac_kernel<NL, 5>), g, b, s, A);
         else if (A.wpe == 1) HB_LAUNCH((hb_wmac_kernel<NL, 0>), g, b, s, A);
-        else HB_LAUNCH((hb_wmac_kernel<NL, (NL >= 64 ? 0 : HB_WMAC_WPE)>), g, b, s, A);
-    }
-    if (A.nblocks > A.nfull) {
-        const u64 n = A.nblocks - A.nfull;
-        HB_LAUNCH((hb_wmac_tail_kernel<NL>), dim3((u32)((n + 63) / 64)), dim3(64), s, A);
+        else HB_LAUNCH((hb_wmac_kernel<NL, HB_WMAC_WPE>), g, b, s, A);
     }
     return hipGetLastError();
 }

@@ -41,15 +41,13 @@ struct WmacArgs {
     ModP<NL> mod;
     const unsigned char *data;    // block k of this launch at data[k C]
     u64 len;
-    u64 nblocks;                  // blocks of the launch
-    u64 nfull;                    // blocks [0, nfull) lie wholly inside the data
+    u64 nfull;                    // blocks [0, nfull): wholly inside the data (the rest: hb_mac_*_kernel)
     u64 C;
     u32 ss, S, tw, Mt, nslices;
     const int8_t *afrag;
     const u32 *kz;                // NL + 1 limbs (device)
     const u32 *fsrc;              // F per block, NL limbs
     unsigned char *tags;          // tw big-endian bytes per block
-    const u32 *alpha_mont;        // the partial-block tail (hb_wmac_tail_kernel): VALU MAC
     u32 wpe;                      // A/B: hb_wmac_kernel's waves-per-SIMD bound (0: the default)
 };
 
