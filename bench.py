@@ -482,9 +482,22 @@ def bench_encode(args, cfg, R):
         line["prove"] = prove_row(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, args, fk, ak,
                                   proofs=args.prove_proofs)
         line["prove"]["seconds_spent"] = round(time.perf_counter() - t, 1)
+    # the host-memory rows come right after the device-resident ones: after
+    # the CPU rows (16 threads streaming 64 GiB through host buffers) the same
+    # rows measured 21-25 instead of 31-38 GiB/s for a real file
+    # (profiles/r05/f: bench_c3 vs bench_c3_nocpu), a state of the process's
+    # host memory, not of the encode
+    want_host = args.host_path or (R.world == 1 and args.config == "c3" and not cxx and not args.single_pass)
+    if R.rank == 0 and want_host and not args.no_host_path:
+        t = time.perf_counter()
+        line["host_path"] = host_path(ctx, L, dptr, pieces[0][1], S, pb, fk, ak, C)
+        line["host_path"]["seconds_spent"] = round(time.perf_counter() - t, 1)
     # the other encode shapes, on prefixes of this very file with tags of
     # their own: PySwizzle's default prime size (1024-bit, S = 10) and
-    # configs[1] (1 GiB, S = 1); rows beside the headline, never `value`
+    # configs[1] (1 GiB, S = 1); rows beside the headline, never `value`.
+    # After the host-memory rows: their parity samples copy ~2 GiB of tags to
+    # host memory, and the API rows measured 23-36 instead of 30-48 GiB/s
+    # behind them (profiles/r06/h)
     if R.rank == 0 and R.world == 1 and args.config == "c3" and not cxx and len(pieces) == 1:
         aes_rate_c3 = aes / (kernel_ms * 1e-3)
         line["aes_g_per_s"] = round(aes_rate_c3 / 1e9, 2)
@@ -498,16 +511,6 @@ def bench_encode(args, cfg, R):
             line["configs1"] = extra_encode_row(ctx, L, dptr, min(1 * GIB, length), 256, 1, fk, ak, args,
                                                 steps=20, warmup=3, aes_rate_ref=aes_rate_c3)
             line["configs1"]["seconds_spent"] = round(time.perf_counter() - t, 1)
-    # the host-memory rows come right after the device-resident ones: after
-    # the CPU rows (16 threads streaming 64 GiB through host buffers) the same
-    # rows measured 21-25 instead of 31-38 GiB/s for a real file
-    # (profiles/r05/f: bench_c3 vs bench_c3_nocpu), a state of the process's
-    # host memory, not of the encode
-    want_host = args.host_path or (R.world == 1 and args.config == "c3" and not cxx and not args.single_pass)
-    if R.rank == 0 and want_host and not args.no_host_path:
-        t = time.perf_counter()
-        line["host_path"] = host_path(ctx, L, dptr, pieces[0][1], S, pb, fk, ak, C)
-        line["host_path"]["seconds_spent"] = round(time.perf_counter() - t, 1)
     if not args.no_parity_sample:
         ok, n = parity_sample(ctx, L, dptr, tptr, pieces, plan, S, p, fk, ak, C, w, args, cxx, fill)
         n_all = int(R.reduce(n, "sum"))
