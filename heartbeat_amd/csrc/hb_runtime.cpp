@@ -1012,8 +1012,14 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // advantage longer (their two-pass retry chains are 2-4x longer): up to
     // 32 x 256 x #CUs blocks for NL >= 16 -- 512-bit S = 16, 2^20 + 1 blocks
     // 3.73 vs 5.01 ms; 1024-bit S = 10, 1.68 M blocks 11.0 vs 11.6, but 2.5 M
-    // 15.7 vs 15.3 (profiles/r05/mid/wide_*.log).  $HB_MID_BLOCKS (test
-    // switch, A/B): another bound, 0 = none.
+    // 15.7 vs 15.3 (profiles/r05/mid/wide_*.log).  Round 6 gave both paths
+    // of the wide primes the MFMA MAC (hb_wmac_kernel): mid vs two-pass
+    // 1024-bit S = 10 1 GiB 4.83 vs 6.73 ms, 2 GiB 7.92 vs 8.32; 512-bit
+    // S = 16 1.2 GiB 3.22 vs 3.72; 2048-bit S = 4 1 GiB 7.20 vs 8.82
+    // (profiles/r06/r6j) -- fits of both (mid ~ 4.7 / 2.6 / 6.9 ms per M
+    // blocks, two-pass ~ 4.1 / 2.0 / 4.0 ms + 2.8 / 1.3 / 4.6 per M) cross
+    // at 2.2 / 1.6 / 1.7 M blocks, next to the 2.1 M bound below.
+    // $HB_MID_BLOCKS (test switch, A/B): another bound, 0 = none.
     const char *mid_env = sw_env(c, "HB_MID_BLOCKS");
     const u64 mid_max = mid_env ? strtoull(mid_env, nullptr, 10) : (NL <= 8 ? 17ull : 32ull) * 256ull * (u64)c->num_cus;
     const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max &&
@@ -1099,16 +1105,17 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(c->vals.ensure((size_t)launch_blocks * NL * 4), "hipMalloc(F)");
         A.fv = (const u32 *)c->vals.p;
     }
-    // split wide-prime encode (wide_plan): F into the tag slots when they are
-    // exactly NL limbs wide and 16-byte aligned, else into c->vals
+    // split wide-prime MAC (wide_plan), two-pass or small / mid-size inputs:
+    // the two-pass F into the tag slots when they are exactly NL limbs wide
+    // and 16-byte aligned, else into c->vals (the small path's F is there)
     WtabArgs<NL> WT;
     memset(&WT, 0, sizeof WT);
     bool wide = false;
     bool f_in_tags = false;
     if constexpr (NL >= 16) {
         u32 w = 0;
-        wide = two_pass && !cxx && (!data_dev || (uintptr_t)data % 16 == 0) && wide_plan<NL>(pi, C, WT, w) &&
-               !sw_env(c, "HB_NO_WIDE");
+        wide = (two_pass || small) && !cxx && (!data_dev || (uintptr_t)data % 16 == 0) &&
+               wide_plan<NL>(pi, C, WT, w) && !sw_env(c, "HB_NO_WIDE");
         if (wide) {
             if (int rc2 = wide_prep<NL>(c, p, pi, w, WT)) return rc2;
             const size_t fbytes = (size_t)WT.nslices * WT.Mt * 64 * 16;
@@ -1119,7 +1126,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             WT.afrag = (int8_t *)c->wtab.p;
             WT.kz = (u32 *)((uint8_t *)c->wtab.p + fbytes);
             WT.status = (unsigned int *)(WT.kz + NL + 1);
-            f_in_tags = pi.tw == 4u * NL && (uintptr_t)dtags % 16 == 0;
+            f_in_tags = two_pass && pi.tw == 4u * NL && (uintptr_t)dtags % 16 == 0;
             if (!f_in_tags) HB_CHECK(c->vals.ensure((size_t)launch_blocks * NL * 4), "hipMalloc(F)");
             mark("wide tables");
         }
@@ -1160,13 +1167,62 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(hb_launch_prefix(PA, nr, c->num_cus, c->stream), "hb_prefix_kernel launch");
         c->last_launches++;
     }
-    if constexpr (NL >= 16) {
-        if (wide) {
-            // the digit table and kz from alpha_j R mod p (on the device, in stream order)
-            HB_CHECK(hipMemsetAsync(WT.status, 0, 4, c->stream), "hipMemsetAsync");
-            HB_CHECK(hb_launch_wtab<NL>(WT, c->stream), "hb_wtab_kernel launch");
-            c->last_launches++;
+    // the digit table and kz from alpha_j R mod p (on the device, in stream
+    // order): here for the two-pass encode, after the first PRF launch for
+    // the small path (whose alpha that launch computes)
+    bool wtab_pending = wide;
+    auto wide_table = [&]() -> int {
+        if constexpr (NL >= 16) {
+            if (wtab_pending) {
+                HB_CHECK(hipMemsetAsync(WT.status, 0, 4, c->stream), "hipMemsetAsync");
+                HB_CHECK(hb_launch_wtab<NL>(WT, c->stream), "hb_wtab_kernel launch");
+                c->last_launches++;
+                wtab_pending = false;
+            }
         }
+        return 0;
+    };
+    // tag = (F + sum_j alpha_j m_j) mod p of a launch's blocks from their F
+    // (fsrc): hb_wmac_kernel for the whole blocks, the sector-parallel MAC
+    // kernel for the short last one (and any past the end of the data)
+    auto wide_mac = [&](const uint8_t *d, u64 dlen, u64 nb, uint8_t *tg, const u32 *fsrc, int align) -> int {
+        if constexpr (NL >= 16) {
+            WmacArgs<NL> M;
+            memset(&M, 0, sizeof M);
+            M.mod = A.mod;
+            M.data = d;
+            M.len = dlen;
+            M.nfull = dlen / C < nb ? dlen / C : nb;
+            M.C = C;
+            M.ss = pi.ss;
+            M.S = S;
+            M.tw = pi.tw;
+            M.Mt = WT.Mt;
+            M.nslices = WT.nslices;
+            M.afrag = WT.afrag;
+            M.kz = WT.kz;
+            M.fsrc = fsrc;
+            M.tags = tg;
+            if (const char *v = sw_env(c, "HB_WMAC_WPE")) M.wpe = (u32)atoi(v);
+            HB_CHECK(hb_launch_wmac<NL>(M, c->stream), "hb_wmac_kernel launch");
+            c->last_launches += M.nfull ? 1 : 0;
+            if (nb > M.nfull) {
+                EncodeArgs<NL> T = A;
+                T.data = d + M.nfull * C;
+                T.len = dlen - M.nfull * C;
+                T.nblocks = nb - M.nfull;
+                T.tags = tg + M.nfull * pi.tw;
+                T.fv = fsrc + M.nfull * NL;
+                HB_CHECK(hb_launch_mac<NL>(T, full16(pi, NL, C, T.data) ? 16 : 1, c->stream), "hb_mac_kernel launch");
+                c->last_launches++;
+            }
+        }
+        (void)d; (void)dlen; (void)nb; (void)tg; (void)fsrc; (void)align;
+        return 0;
+    };
+    if (two_pass) {
+        rc = wide_table();
+        if (rc) return rc;
     }
     if (mf_layout) {
         // built on the host while the GPU runs the prefix kernel
@@ -1237,8 +1293,14 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             } else {
                 HB_CHECK(hb_launch_prf<NL>(F, nr, 3, es.grid, c->stream), "hb_prf_kernel launch");
             }
+            c->last_launches++;
+            if (wide) {
+                rc = wide_table();
+                if (!rc) rc = wide_mac(d, dlen, nb, tg, (const u32 *)c->vals.p, align);
+                return rc;
+            }
             HB_CHECK(hb_launch_mac<NL>(A, align, c->stream), "hb_mac_kernel launch");
-            c->last_launches += 2;
+            c->last_launches++;
             return 0;
         }
         // queue[0] is the per-launch job counter (and queue[3] the retry
@@ -1266,42 +1328,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         if (data_dev) HB_CHECK(hipEventRecord(c->ph[2], c->stream), "hipEventRecord");
         c->ph_valid = data_dev;
         c->last_launches += 2;
-        if constexpr (NL >= 16) {
-            if (wide) {
-                WmacArgs<NL> M;
-                memset(&M, 0, sizeof M);
-                M.mod = A.mod;
-                M.data = d;
-                M.len = dlen;
-                M.nfull = dlen / C < nb ? dlen / C : nb;
-                M.C = C;
-                M.ss = pi.ss;
-                M.S = S;
-                M.tw = pi.tw;
-                M.Mt = WT.Mt;
-                M.nslices = WT.nslices;
-                M.afrag = WT.afrag;
-                M.kz = WT.kz;
-                M.fsrc = A.fout;
-                M.tags = tg;
-                if (const char *v = sw_env(c, "HB_WMAC_WPE")) M.wpe = (u32)atoi(v);
-                HB_CHECK(hb_launch_wmac<NL>(M, c->stream), "hb_wmac_kernel launch");
-                c->last_launches += M.nfull ? 1 : 0;
-                if (nb > M.nfull) {
-                    // the short last block (and any past the end of the data):
-                    // the small path's MAC kernel, the block's sectors over lanes
-                    EncodeArgs<NL> T = A;
-                    T.data = d + M.nfull * C;
-                    T.len = dlen - M.nfull * C;
-                    T.nblocks = nb - M.nfull;
-                    T.tags = tg + M.nfull * pi.tw;
-                    T.fv = A.fout + M.nfull * NL;
-                    HB_CHECK(hb_launch_mac<NL>(T, full16(pi, NL, C, T.data) ? 16 : 1, c->stream),
-                             "hb_mac_kernel launch");
-                    c->last_launches++;
-                }
-            }
-        }
+        if (wide) return wide_mac(d, dlen, nb, tg, A.fout, align);
         return 0;
     };
 
