@@ -523,6 +523,12 @@ struct EncodeHandler {
     __device__ __forceinline__ void init(u64, u32 sr[4]) const { hb_zero_sr(sr); }
     __device__ __forceinline__ void accept(u64 job, const u32 F[NL]) const {
         if constexpr (ALIGN == 0) {   // split wide-prime encode: F for hb_wmac_kernel
+            if (MODE == 1 && job * A.C >= A.len) {
+                // cxx, no sector read: the tag is F itself, unreduced
+                // (shacham_waters_private.cxx:681-690); no MAC kernel reads it
+                hb_store_be<NL>(A.tags + job * (u64)A.tw, A.tw, F);
+                return;
+            }
             hb_store_limbs<NL>(A.fout + job * NL, F);
         } else {
 #if defined(HB_EXP_NO_MAC)
@@ -2145,7 +2151,7 @@ hipError_t hb_launch_encode_pass(const EncodeArgs<NL> &A, int nr, int align, int
     } while (0)
     if constexpr (PASS == 1) HB_ENC_AL0(hb_encode_first_kernel);
     else if constexpr (PASS == 2) HB_ENC_AL0(hb_encode_retry_kernel);
-    else if constexpr (PASS == 3) HB_ENC_AL(hb_cxx_encode_kernel);
+    else if constexpr (PASS == 3) HB_ENC_AL0(hb_cxx_encode_kernel);
     else HB_ENC_AL(hb_encode_kernel);
 #undef HB_ENC_AL0
 #undef HB_ENC_AL

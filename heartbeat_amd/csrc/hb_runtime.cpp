@@ -399,7 +399,7 @@ void prepare_nl(hb_ctx *c) {
     for (int pass = 0; pass <= 3; ++pass)
         for (int align : {16, 1}) (void)hb_launch_encode<NL>(E, 14, align, pass, 0, c->stream);
     if constexpr (NL >= 16) {   // the split wide-prime encode (wide_plan)
-        for (int pass = 1; pass <= 2; ++pass) (void)hb_launch_encode<NL>(E, 14, 0, pass, 0, c->stream);
+        for (int pass = 1; pass <= 3; ++pass) (void)hb_launch_encode<NL>(E, 14, 0, pass, 0, c->stream);
         WtabArgs<NL> WT;
         memset(&WT, 0, sizeof WT);
         (void)hb_launch_wtab<NL>(WT, c->stream);
@@ -1114,8 +1114,9 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     bool f_in_tags = false;
     if constexpr (NL >= 16) {
         u32 w = 0;
-        wide = (two_pass || small) && !cxx && (!data_dev || (uintptr_t)data % 16 == 0) &&
-               wide_plan<NL>(pi, C, WT, w) && !sw_env(c, "HB_NO_WIDE");
+        // (the cxx prf: its single-pass engine, F-only as well)
+        wide = (two_pass || small || (cxx && !(flags & HB_ENCODE_SINGLE_PASS))) &&
+               (!data_dev || (uintptr_t)data % 16 == 0) && wide_plan<NL>(pi, C, WT, w) && !sw_env(c, "HB_NO_WIDE");
         if (wide) {
             if (int rc2 = wide_prep<NL>(c, p, pi, w, WT)) return rc2;
             const size_t fbytes = (size_t)WT.nslices * WT.Mt * 64 * 16;
@@ -1126,7 +1127,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             WT.afrag = (int8_t *)c->wtab.p;
             WT.kz = (u32 *)((uint8_t *)c->wtab.p + fbytes);
             WT.status = (unsigned int *)(WT.kz + NL + 1);
-            f_in_tags = two_pass && pi.tw == 4u * NL && (uintptr_t)dtags % 16 == 0;
+            f_in_tags = !small && pi.tw == 4u * NL && (uintptr_t)dtags % 16 == 0;
             if (!f_in_tags) HB_CHECK(c->vals.ensure((size_t)launch_blocks * NL * 4), "hipMalloc(F)");
             mark("wide tables");
         }
@@ -1185,6 +1186,8 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // tag = (F + sum_j alpha_j m_j) mod p of a launch's blocks from their F
     // (fsrc): hb_wmac_kernel for the whole blocks, the sector-parallel MAC
     // kernel for the short last one (and any past the end of the data)
+    // (cxx: blocks without a sector read hold their final tag already, F
+    // unreduced, from the PRF kernel -- the MAC kernels stop before them)
     auto wide_mac = [&](const uint8_t *d, u64 dlen, u64 nb, uint8_t *tg, const u32 *fsrc, int align) -> int {
         if constexpr (NL >= 16) {
             WmacArgs<NL> M;
@@ -1206,11 +1209,13 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             if (const char *v = sw_env(c, "HB_WMAC_WPE")) M.wpe = (u32)atoi(v);
             HB_CHECK(hb_launch_wmac<NL>(M, c->stream), "hb_wmac_kernel launch");
             c->last_launches += M.nfull ? 1 : 0;
-            if (nb > M.nfull) {
+            const u64 with_data = (dlen + C - 1) / C < nb ? (dlen + C - 1) / C : nb;
+            const u64 tail_end = cxx ? with_data : nb;
+            if (tail_end > M.nfull) {
                 EncodeArgs<NL> T = A;
                 T.data = d + M.nfull * C;
                 T.len = dlen - M.nfull * C;
-                T.nblocks = nb - M.nfull;
+                T.nblocks = tail_end - M.nfull;
                 T.tags = tg + M.nfull * pi.tw;
                 T.fv = fsrc + M.nfull * NL;
                 HB_CHECK(hb_launch_mac<NL>(T, full16(pi, NL, C, T.data) ? 16 : 1, c->stream), "hb_mac_kernel launch");
@@ -1220,7 +1225,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         (void)d; (void)dlen; (void)nb; (void)tg; (void)fsrc; (void)align;
         return 0;
     };
-    if (two_pass) {
+    if (!small) {
         rc = wide_table();
         if (rc) return rc;
     }
@@ -1308,9 +1313,11 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         HB_CHECK(hipMemsetAsync(q0, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");
         if (!two_pass) {
             A.queue = q0;
-            HB_CHECK(hb_launch_encode<NL>(A, nr, align, cxx ? 3 : 0, engine_grid(c, nb), c->stream),
+            if (wide) A.fout = f_in_tags ? (u32 *)tg : (u32 *)c->vals.p;
+            HB_CHECK(hb_launch_encode<NL>(A, nr, wide ? 0 : align, cxx ? 3 : 0, engine_grid(c, nb), c->stream),
                      "hb_encode_kernel launch");
             c->last_launches++;
+            if (wide) return wide_mac(d, dlen, nb, tg, A.fout, align);
             return 0;
         }
         HB_CHECK(hipMemsetAsync(q0 + 3, 0, sizeof(unsigned long long), c->stream), "hipMemsetAsync");

@@ -28,7 +28,10 @@ def prime(bits):
 
 
 out = []
-for bits, S, gib in [(0 if a == "P256" else int(a), int(b), float(c)) for a, b, c in (x.split(":") for x in sys.argv[1:])]:
+# bits:S:GiB[:cxx] -- ":cxx" encodes with the cxx Swizzle prf (HB_PRF_CXX;
+# its oracle restatement is parity unpinned)
+for bits, S, gib, cxx in [(0 if a[0] == "P256" else int(a[0]), int(a[1]), float(a[2]), a[3:] == ["cxx"])
+                          for a in (x.split(":") for x in sys.argv[1:])]:
     p = prime(bits)
     w = nat.width_of(p)
     C = (p.bit_length() // 8) * S
@@ -46,7 +49,8 @@ for bits, S, gib in [(0 if a == "P256" else int(a), int(b), float(c)) for a, b, 
     best = None
     for rep in range(4):
         t0 = time.perf_counter()
-        ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, d, n, nb, t, 3, None))
+        ctx.check(L.hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, d, n, nb, t, 3 | (nat.HB_PRF_CXX if cxx else 0),
+                              None))
         dt = time.perf_counter() - t0
         kms = ctx.last_kernel_ms()[0]
         if rep and (best is None or dt < best[0]):
@@ -60,10 +64,10 @@ for bits, S, gib in [(0 if a == "P256" else int(a), int(b), float(c)) for a, b, 
             ctx.check(L.hb_memcpy(ctx.h, blk.ctypes.data, d.value + b * C, m, 2))
         tg = np.empty(w, dtype=np.uint8)
         ctx.check(L.hb_memcpy(ctx.h, tg.ctypes.data, t.value + b * w, w, 2))
-        want = O.encode(p, S, fk, ak, blk.tobytes()[:m], block_base=b, nblocks=1)[0]
+        want = (O.cxx_encode if cxx else O.encode)(p, S, fk, ak, blk.tobytes()[:m], block_base=b, nblocks=1)[0]
         ok = ok and int.from_bytes(tg.tobytes(), "big") == want
     ctx.check(L.hb_device_free(ctx.h, d))
     ctx.check(L.hb_device_free(ctx.h, t))
-    out.append({"prime_bits": bits or "P256", "sectors": S, "gib": gib, "blocks": nb, "gib_s": round(n / (1 << 30) / best[0], 2),
+    out.append({"prime_bits": bits or "P256", "sectors": S, "gib": gib, "prf": "cxx" if cxx else "pyswizzle", "blocks": nb, "gib_s": round(n / (1 << 30) / best[0], 2),
                 "wall_ms": round(best[0] * 1e3, 3), "kernel_ms": round(best[1], 3), "sample_equal_oracle": ok})
     print(json.dumps(out[-1]), flush=True)

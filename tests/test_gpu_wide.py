@@ -169,3 +169,44 @@ def test_split_4gib_defaults_sampled(nat, oracle, monkeypatch):
         m = min(C, max(0, n - b * C))
         blk = splitmix_bytes(4242, b * C, m)
         assert got[b] == oracle.encode(p, S, fk, ak, blk, block_base=b, nblocks=1)[0], b
+
+
+@pytest.mark.parametrize("nbytes", [8 << 20, (8 << 20) + 333, 1280 * 5000, 100])
+def test_split_cxx_prf_equals_inkernel_mac_and_oracle(nat, oracle, monkeypatch, nbytes):
+    """The cxx Swizzle encode (cxx prf, single-pass engine) at its API's
+    1024-bit prime, S = 10, through the split MAC == its in-kernel VALU MAC
+    ($HB_NO_WIDE) == the oracle's cxx restatement (parity of the cxx mode
+    itself is unpinned: no Crypto++).  1280 x 5000 bytes ends on a block
+    boundary, so the last block has no sector read and keeps F unreduced
+    (shacham_waters_private.cxx:681-690).  Reference: :638-702."""
+    p = _prime(1024, 99)
+    S, C, w = 10, 1280, 128
+    nb = nbytes // C + 1
+    data = np.random.default_rng(nbytes).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+    fk, ak = hashlib.sha256(b"cx-f").digest(), hashlib.sha256(b"cx-a").digest()
+    ctx = nat.context()
+    pb = nat.be(p)
+    buf = DevBuf(nat, max(nbytes, 16))
+    res = []
+    try:
+        buf.upload(data)
+        for no_wide in (False, True):
+            if no_wide:
+                monkeypatch.setenv("HB_NO_WIDE", "1")
+            tb = DevBuf(nat, nb * w)
+            try:
+                ctx.check(nat.lib().hb_encode(ctx.h, pb, len(pb), S, fk, ak, 32, 0, buf.p, nbytes, nb, tb.p,
+                                              3 | nat.HB_PRF_CXX, None))
+                res.append(tb.download())
+            finally:
+                tb.free()
+    finally:
+        monkeypatch.delenv("HB_NO_WIDE", raising=False)
+        buf.free()
+    assert res[0] == res[1]
+    got = split_tags(res[0], w)
+    if nb <= 7000:
+        assert got == oracle.cxx_encode(p, S, fk, ak, data, nthreads=8)
+    else:
+        for b in sorted(set(np.random.default_rng(3).integers(0, nb, 300).tolist()) | {0, nb - 2, nb - 1}):
+            assert got[b] == oracle.cxx_encode(p, S, fk, ak, data[b * C:(b + 1) * C], block_base=b, nblocks=1)[0], b
