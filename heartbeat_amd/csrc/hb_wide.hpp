@@ -200,33 +200,37 @@ void hb_wmac_kernel(WmacArgs<NL> A) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[HbWmac<NL>::LDS_BYTES];
     const u32 l = hb_lane_id(), wv = threadIdx.x >> 6;
     const u64 w0 = (u64)blockIdx.x * NB;
-    // slice loads: piece u = r NT + threadIdx.x, r < NB 4 / NT: block u / 4,
-    // bytes 16 (u % 4) .. + 15 of the slice; stored at LDS unit (g, u % 4, n)
-    // of its group g = (u / 4) / 16, n = (u / 4) % 16 -- lane (q, n) of a wave
-    // reads unit (g, q, n): consecutive lanes, consecutive 16 bytes
+    // slice loads: thread i fills LDS unit u = r NT + i (16 bytes at 16 u),
+    // unit u = (g 4 + q) 16 + n holding bytes 16 q .. + 15 of the slice of
+    // block 16 g + n -- lane (q, n) of a wave reads unit (g, q, n), and the
+    // stores of consecutive lanes land on consecutive 16 bytes (no bank
+    // conflicts; with one thread per 64-byte piece 48 % of the LDS cycles
+    // were conflicts, profiles/r06/r6m).  A wave's load still covers 16
+    // blocks x 64 contiguous bytes.
     constexpr int LR = NB * 4 / NT;   // 16-byte pieces per thread per slice
     const unsigned char *src[LR];
     bool okp[LR];
-    u32 dst[LR];
+    u32 qof[LR];
 #pragma unroll
     for (int r = 0; r < LR; ++r) {
-        const u32 u = (u32)r * NT + threadIdx.x, b = u >> 2, qq = u & 3u;
+        const u32 u = (u32)r * NT + threadIdx.x, b = ((u >> 6) << 4) | (u & 15u), qq = (u >> 4) & 3u;
         const u64 blk = w0 + b;
         okp[r] = blk < A.nfull;
+        qof[r] = 16u * qq;
         src[r] = A.data + (okp[r] ? blk : w0) * A.C + 16u * qq;
-        dst[r] = (((b >> 4) * 4u + qq) * 16u + (b & 15u)) * 16u;
     }
     auto gload = [&](u32 s, hb_i32x4 v[LR]) {
 #pragma unroll
         for (int r = 0; r < LR; ++r) {
-            const bool in = okp[r] && 64u * s + 16u * ((threadIdx.x + (u32)r * NT) & 3u) < A.C;
+            const bool in = okp[r] && 64u * s + qof[r] < A.C;
             v[r] = in ? *reinterpret_cast<const hb_i32x4 *>(src[r] + 64u * s) : hb_i32x4{0, 0, 0, 0};
         }
     };
     auto lstore = [&](u32 buf, const hb_i32x4 v[LR]) {
 #pragma unroll
         for (int r = 0; r < LR; ++r)
-            *reinterpret_cast<hb_i32x4 *>(lds + buf * (NB * 64) + dst[r]) = v[r] ^ (int32_t)0x80808080;
+            *reinterpret_cast<hb_i32x4 *>(lds + buf * (NB * 64) + 16u * ((u32)r * NT + threadIdx.x)) =
+                v[r] ^ (int32_t)0x80808080;
     };
     const u32 t0 = wv * (u32)TW;
     const bool mine = t0 < A.Mt;   // wave-uniform: this wave has tiles
