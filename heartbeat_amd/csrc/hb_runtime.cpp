@@ -120,6 +120,12 @@ struct hb_ctx {
     // the alpha D2H into hscratch done / the MFMA-table H2D out of it done
     // (not yet waited for: the next round trip must wait before reusing hscratch)
     hipEvent_t ev_alpha = nullptr, ev_h2d = nullptr;
+    // split wide-prime encode: alpha's PRF, its Montgomery form and the digit
+    // table run on `side` beside the prefix image and the PRF passes (which do
+    // not read alpha); ev_side0 orders them after the stream's earlier work,
+    // ev_side1 orders the MAC after them
+    hipStream_t side = nullptr;
+    hipEvent_t ev_side0 = nullptr, ev_side1 = nullptr;
     bool h2d_pending = false;
     bool alpha_pending = false;   // the alpha D2H into hscratch not yet waited for
     bool prove_dirty = false;   // a prove stopped between its launches: counters to clear
@@ -211,6 +217,7 @@ const SwitchName kSwitches[] = {
     {"HB_MID_BLOCKS", HB_SW_MID_BLOCKS},
     {"HB_NO_WIDE", HB_SW_NO_WIDE},
     {"HB_WMAC_WPE", HB_SW_WMAC_WPE},
+    {"HB_WIDE_SYNC_ALPHA", HB_SW_WIDE_SYNC_ALPHA},
 };
 
 int nl_for_bits(int bits) {
@@ -306,7 +313,8 @@ int check_key(hb_ctx *c, size_t key_len) {
 template <int NL>
 int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_be, size_t range_len,
             const u64 *xs_dev, u64 x0, u64 n, u32 *out_dev, int queue_slot, int mode = 0,
-            const u32 *digs_dev = nullptr) {
+            const u32 *digs_dev = nullptr, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     PrfArgs<NL> A;
     int nr = 0;
     if (!make_prf<NL>(key, key_len, range_be, range_len, A.prf, nr))
@@ -325,8 +333,8 @@ int run_prf(hb_ctx *c, const uint8_t *key, size_t key_len, const uint8_t *range_
     // quad waves placed by SIMD as in the prove (hb_prove_place; every quad
     // launch's waves fit: use_quad); $HB_NO_PROVE_PLACE: the job-queue race
     A.place = quad && !sw_env(c, "HB_NO_PROVE_PLACE") ? 1u : 0u;
-    HB_CHECK(hipMemsetAsync(A.queue, 0, HB_QSLOT * sizeof(unsigned long long), c->stream), "hipMemsetAsync");
-    HB_CHECK(hb_launch_prf<NL>(A, nr, quad ? 3 : mode, es.grid, c->stream), "hb_prf_kernel launch");
+    HB_CHECK(hipMemsetAsync(A.queue, 0, HB_QSLOT * sizeof(unsigned long long), st), "hipMemsetAsync");
+    HB_CHECK(hb_launch_prf<NL>(A, nr, quad ? 3 : mode, es.grid, st), "hb_prf_kernel launch");
     return 0;
 }
 
@@ -341,7 +349,8 @@ int check_prf_slots(hb_ctx *c) {
 
 // in (n x NL limbs, device) -> in * R mod p (device)
 template <int NL>
-int run_mont(hb_ctx *c, const Limbs &p, const u32 *in, u32 *out, u64 n) {
+int run_mont(hb_ctx *c, const Limbs &p, const u32 *in, u32 *out, u64 n, hipStream_t st = nullptr) {
+    if (!st) st = c->stream;
     if (n == 0) return 0;
     MontArgs<NL> A;
     make_mod<NL>(p, A.mod);
@@ -350,7 +359,7 @@ int run_mont(hb_ctx *c, const Limbs &p, const u32 *in, u32 *out, u64 n) {
     A.in = in;
     A.out = out;
     A.n = n;
-    HB_CHECK(hb_launch_mont<NL>(A, c->stream), "hb_mont_kernel launch");
+    HB_CHECK(hb_launch_mont<NL>(A, st), "hb_mont_kernel launch");
     return 0;
 }
 
@@ -1025,14 +1034,6 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max &&
                        (use_quad(c, launch_max + S) || launch_max <= mid_max) && !sw_env(c, "HB_NO_SMALL_ENCODE");
     int rc = 0;
-    if (!small) {
-        rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, cxx ? 1 : 0);
-        if (rc) return rc;
-        mark("alpha PRF");
-        rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S);
-        if (rc) return rc;
-        mark("alpha PRF + Montgomery");
-    }
 
     EncodeArgs<NL> A;
     memset(&A, 0, sizeof A);
@@ -1132,6 +1133,24 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             mark("wide tables");
         }
     }
+    // alpha_j R mod p (large inputs; the small path's first launch computes
+    // it): on the compute stream, or for the split wide-prime encode on the
+    // side stream together with the digit table (wide_table below)
+    const bool side = !small && wide && !sw_env(c, "HB_WIDE_SYNC_ALPHA");
+    hipStream_t ast = side ? c->side : c->stream;
+    if (side) {
+        HB_CHECK(hipEventRecord(c->ev_side0, c->stream), "hipEventRecord");
+        HB_CHECK(hipStreamWaitEvent(c->side, c->ev_side0, 0), "hipStreamWaitEvent");
+    }
+    if (!small) {
+        rc = run_prf<NL>(c, a_key, key_len, p_be, p_len, nullptr, 0, S, (u32 *)c->alpha_raw.p, 1, cxx ? 1 : 0,
+                         nullptr, ast);
+        if (rc) return rc;
+        mark("alpha PRF");
+        rc = run_mont<NL>(c, p, (const u32 *)c->alpha_raw.p, (u32 *)c->alpha_mont.p, S, ast);
+        if (rc) return rc;
+        mark("alpha PRF + Montgomery");
+    }
     if (two_pass) {
         A.retry_cap = retry_capacity(c, p_be, p_len, launch_blocks);
         HB_CHECK(c->retry.ensure((size_t)(A.retry_cap ? A.retry_cap : 1) * sizeof(HbRetry)), "hipMalloc(retry)");
@@ -1175,8 +1194,9 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     auto wide_table = [&]() -> int {
         if constexpr (NL >= 16) {
             if (wtab_pending) {
-                HB_CHECK(hipMemsetAsync(WT.status, 0, 4, c->stream), "hipMemsetAsync");
-                HB_CHECK(hb_launch_wtab<NL>(WT, c->stream), "hb_wtab_kernel launch");
+                HB_CHECK(hipMemsetAsync(WT.status, 0, 4, ast), "hipMemsetAsync");
+                HB_CHECK(hb_launch_wtab<NL>(WT, ast), "hb_wtab_kernel launch");
+                if (side) HB_CHECK(hipEventRecord(c->ev_side1, c->side), "hipEventRecord");
                 c->last_launches++;
                 wtab_pending = false;
             }
@@ -1207,6 +1227,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
             M.fsrc = fsrc;
             M.tags = tg;
             if (const char *v = sw_env(c, "HB_WMAC_WPE")) M.wpe = (u32)atoi(v);
+            if (side) HB_CHECK(hipStreamWaitEvent(c->stream, c->ev_side1, 0), "hipStreamWaitEvent");
             HB_CHECK(hb_launch_wmac<NL>(M, c->stream), "hb_wmac_kernel launch");
             c->last_launches += M.nfull ? 1 : 0;
             const u64 with_data = (dlen + C - 1) / C < nb ? (dlen + C - 1) / C : nb;
@@ -2172,6 +2193,9 @@ int hb_ctx_create(int device, hb_ctx **out) {
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
     c->own_stream = c->stream;
     if ((e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    if ((e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess) return bad(e, "hipStreamCreate");
+    if ((e = hipEventCreateWithFlags(&c->ev_side0, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&c->ev_side1, hipEventDisableTiming)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreate(&c->k0)) != hipSuccess) return bad(e, "hipEventCreate");
     if ((e = hipEventCreate(&c->k1)) != hipSuccess) return bad(e, "hipEventCreate");
     for (int k = 0; k < 3; ++k)
@@ -2200,6 +2224,7 @@ void hb_ctx_destroy(hb_ctx *c) {
     settle(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     DevBuf *bufs[] = {&c->alpha_raw, &c->alpha_mont, &c->xs, &c->vals, &c->vals2, &c->wts, &c->idx,
                       &c->partials, &c->sums, &c->data[0], &c->data[1], &c->tags, &c->blen, &c->gtags,
                       &c->pfx, &c->retry, &c->ctl, &c->afrag, &c->mseeds, &c->moffs, &c->mdig, &c->gdev,
@@ -2223,6 +2248,9 @@ void hb_ctx_destroy(hb_ctx *c) {
     }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->copy) (void)hipStreamDestroy(c->copy);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->ev_side0) (void)hipEventDestroy(c->ev_side0);
+    if (c->ev_side1) (void)hipEventDestroy(c->ev_side1);
     delete c;
 }
 
