@@ -1,7 +1,7 @@
 """Provenance of the committed measurement records (CPU): the traffic figure
 bench.py quotes (profiles/pmc_traffic.json, roofline.traffic) is exactly what
 scripts/pmc_traffic.py derives from the committed rocprofv3 --pmc passes it
-names, and every profile file DESIGN.md cites for rounds 4 and 5 exists."""
+names, and every profile file DESIGN.md cites for rounds 4 to 6 exists."""
 import json
 import os
 import re
@@ -22,9 +22,9 @@ def test_pmc_traffic_reproduces_from_committed_passes():
         assert again[k] == rec[k], k
 
 
-def test_design_cites_existing_round4_and_round5_profiles():
+def test_design_cites_existing_round4_to_round6_profiles():
     text = open(os.path.join(ROOT, "DESIGN.md")).read()
-    for rnd in ("r04", "r05"):
+    for rnd in ("r04", "r05", "r06"):
         cited = set(re.findall(r"`(profiles/%s/[^`*{}\n]+?)`" % rnd, text))
         assert cited, rnd
         missing = [c for c in cited if not os.path.exists(os.path.join(ROOT, c.rstrip("/").split(" ")[0]))]
