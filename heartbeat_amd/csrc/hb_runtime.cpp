@@ -994,6 +994,10 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
         fprintf(stderr, "[hb_encode] %-28s %9.3f ms\n", what,
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
     };
+    // the side stream's work of an earlier split encode reads the alpha and
+    // table buffers regrown below; it has finished unless that call failed
+    // between its launches (the MAC waits for it otherwise)
+    HB_CHECK(hipStreamSynchronize(c->side), "hipStreamSynchronize(side)");
     // alpha_j R mod p, j < S  (alpha = KeyedPRF(alpha_key, p), PySwizzle.py:291,302)
     HB_CHECK(c->alpha_raw.ensure((size_t)S * NL * 4), "hipMalloc");
     HB_CHECK(c->alpha_mont.ensure((size_t)S * NL * 4), "hipMalloc");
