@@ -103,6 +103,9 @@ struct EncodeArgs {
     // split wide-prime encode (PRF kernels with ALIGN = 0): F(block_base + k)
     // as NL little-endian limbs at fout + k NL, for hb_wmac_kernel
     u32 *fout;
+    // jobs per queue refill in the first / retry passes and the single-pass
+    // engine (0: HB_QUEUE_CHUNK; hb_runtime.cpp encode_qchunk)
+    u64 qchunk;
 };
 
 // The split wide-prime encode's argument blocks: hb_wide_args.hpp.

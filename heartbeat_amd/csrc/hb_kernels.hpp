@@ -61,6 +61,8 @@ __device__ __forceinline__ u64 hb_bcast64(u64 v) {
     return ((u64)hi << 32) | lo;
 }
 
+__device__ __forceinline__ u64 hb_qchunk(u64 q) { return q ? q : (u64)HB_QUEUE_CHUNK; }
+
 // Wave-local job pool over a global counter.  All members are wave-uniform.
 struct HbPool {
     u64 next, end, njobs;
@@ -393,8 +395,8 @@ __device__ __forceinline__ void hb_engine_quad(H &h, const LaneTab &L, const Prf
 #endif
 template <int NL, int NR, class H>
 __device__ __forceinline__ void hb_engine_tail(H &h, const LaneTab &L, const PrfParams<NL> &P, u64 njobs,
-                                               unsigned long long *queue) {
-    HbPool pool{0, 0, njobs, queue, false, HB_QUEUE_CHUNK};
+                                               unsigned long long *queue, u64 chunk) {
+    HbPool pool{0, 0, njobs, queue, false, chunk};
     u64 job = 0;
     bool active = pool.take(__ballot(1), true, job);
     u32 dig[8], sr[4] = {0, 0, 0, 0}, out[NL];
@@ -554,7 +556,7 @@ __global__ __launch_bounds__((HbEncWg<NL, ALIGN>::v), HbEncodeOcc<NL>::v) void h
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     EncodeHandler<NL, ALIGN> h{A};
-    hb_engine<NL, NR>(h, L, A.prf, A.nblocks, A.queue);
+    hb_engine<NL, NR>(h, L, A.prf, A.nblocks, A.queue, hb_qchunk(A.qchunk));
 }
 
 // Small inputs (hb_runtime.cpp: as many blocks as the quad engine runs at
@@ -633,7 +635,7 @@ __global__ __launch_bounds__((HbEncWg<NL, ALIGN>::v), HbEncodeOcc<NL>::v) void h
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     EncodeHandler<NL, ALIGN, 1> h{A};
-    hb_engine<NL, NR, EncodeHandler<NL, ALIGN, 1>, 1>(h, L, A.prf, A.nblocks, A.queue);
+    hb_engine<NL, NR, EncodeHandler<NL, ALIGN, 1>, 1>(h, L, A.prf, A.nblocks, A.queue, hb_qchunk(A.qchunk));
 }
 
 // ------------------------------------------------------------------ two-pass encode
@@ -1118,7 +1120,7 @@ __global__ __launch_bounds__((HbEncWg<NL, ALIGN>::v), HbEncodeOcc<NL>::v) void h
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     EncodeHandler<NL, ALIGN> h{A};
-    HbPool pool{0, 0, A.nblocks, A.queue, false, HB_QUEUE_CHUNK};
+    HbPool pool{0, 0, A.nblocks, A.queue, false, hb_qchunk(A.qchunk)};
     u32 tries = 0, failed = 0;
     for (;;) {
         u64 job = 0;
@@ -1231,8 +1233,8 @@ __global__ __launch_bounds__((HbEncWg<NL, ALIGN>::v), HbEncodeOcc<NL>::v) void h
     hb_fill_lds(lds, A.t0);
     const LaneTab L = hb_lane_tab(lds);
     RetryHandler<NL, ALIGN> h{A};
-    if constexpr ((NL == 8 || ALIGN == 0) && HB_RETRY_QUAD_TAIL) hb_engine_tail<NL, NR>(h, L, A.prf, n, A.queue);
-    else hb_engine<NL, NR>(h, L, A.prf, n, A.queue);
+    if constexpr ((NL == 8 || ALIGN == 0) && HB_RETRY_QUAD_TAIL) hb_engine_tail<NL, NR>(h, L, A.prf, n, A.queue, hb_qchunk(A.qchunk));
+    else hb_engine<NL, NR>(h, L, A.prf, n, A.queue, hb_qchunk(A.qchunk));
 }
 
 // r (NL limbs, < p) += x (NL limbs, < p) mod p

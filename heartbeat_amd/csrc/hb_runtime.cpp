@@ -218,6 +218,7 @@ const SwitchName kSwitches[] = {
     {"HB_NO_WIDE", HB_SW_NO_WIDE},
     {"HB_WMAC_WPE", HB_SW_WMAC_WPE},
     {"HB_WIDE_SYNC_ALPHA", HB_SW_WIDE_SYNC_ALPHA},
+    {"HB_QCHUNK", HB_SW_QCHUNK},
 };
 
 int nl_for_bits(int bits) {
@@ -286,6 +287,17 @@ EngineShape small_engine(hb_ctx *c, u64 njobs) {
     u64 g = (njobs + 63) / 64;   // 64-job chunks: at most one workgroup (CU) each
     if (g > (u64)c->num_cus) g = (u64)c->num_cus;
     return {(int)(g ? g : 1), 64};
+}
+
+// Jobs per queue refill in the encode engines.  $HB_QCHUNK=n (A/B): n,
+// rounded up to a multiple of 64 (HbPool hands a wave at most one refill per
+// take, so a refill must cover all 64 lanes).
+u64 encode_qchunk(hb_ctx *c) {
+    const char *q = sw_env(c, "HB_QCHUNK");
+    if (!q) return HB_QUEUE_CHUNK;
+    u64 n = strtoull(q, nullptr, 10);
+    n = (n + 63) / 64 * 64;
+    return n ? n : 64;
 }
 
 // The quad engine (one KeyedPRF evaluation per four lanes, hb_engine_quad)
@@ -1041,6 +1053,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 
     EncodeArgs<NL> A;
     memset(&A, 0, sizeof A);
+    A.qchunk = encode_qchunk(c);
     int mf_layout = 0;   // MFMA MAC table layout (0: VALU MAC)
     if constexpr (NL == 8) {
         // MFMA MAC tables (hb_mfma_block_acc): 256-bit primes with whole
