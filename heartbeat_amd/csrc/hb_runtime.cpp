@@ -289,12 +289,17 @@ EngineShape small_engine(hb_ctx *c, u64 njobs) {
     return {(int)(g ? g : 1), 64};
 }
 
-// Jobs per queue refill in the encode engines.  $HB_QCHUNK=n (A/B): n,
-// rounded up to a multiple of 64 (HbPool hands a wave at most one refill per
-// take, so a refill must cover all 64 lanes).
-u64 encode_qchunk(hb_ctx *c) {
+// Jobs per queue refill in the encode engines: 256 for primes up to 256
+// bits; 64 for the wider ones, whose tries are 64-256 serial AES, so that a
+// pass does not end on a few waves still holding a refill's worth of jobs
+// (8 GiB, 256 -> 64: 1024-bit S = 10 336 -> 360, 512-bit 573 -> 602,
+// 2048-bit 182 -> 195 GiB/s; 256-bit S = 16 within noise, 1,002 vs 987;
+// profiles/r06/r6q).  $HB_QCHUNK=n (A/B): n, rounded up to a multiple of 64
+// (HbPool hands a wave at most one refill per take, so a refill must cover
+// all 64 lanes).
+u64 encode_qchunk(hb_ctx *c, int nl) {
     const char *q = sw_env(c, "HB_QCHUNK");
-    if (!q) return HB_QUEUE_CHUNK;
+    if (!q) return nl >= 16 ? 64 : HB_QUEUE_CHUNK;
     u64 n = strtoull(q, nullptr, 10);
     n = (n + 63) / 64 * 64;
     return n ? n : 64;
@@ -1053,7 +1058,7 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
 
     EncodeArgs<NL> A;
     memset(&A, 0, sizeof A);
-    A.qchunk = encode_qchunk(c);
+    A.qchunk = encode_qchunk(c, NL);
     int mf_layout = 0;   // MFMA MAC table layout (0: VALU MAC)
     if constexpr (NL == 8) {
         // MFMA MAC tables (hb_mfma_block_acc): 256-bit primes with whole

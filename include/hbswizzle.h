@@ -126,7 +126,7 @@ const char *hb_build_flags_string(void);
 #define HB_SW_NO_WIDE 524288u       /* HB_NO_WIDE: primes above 256 bits keep the MAC inside the PRF kernels (VALU) instead of the split F-only passes + MFMA MAC (hb_wmac_kernel) */
 #define HB_SW_WMAC_WPE 1048576u     /* HB_WMAC_WPE=1|3|5: hb_wmac_kernel built for another waves-per-SIMD bound (1: the compiler's choice) */
 #define HB_SW_WIDE_SYNC_ALPHA 2097152u /* HB_WIDE_SYNC_ALPHA: the split encode computes alpha and its digit table on the compute stream, before the PRF passes, instead of beside them */
-#define HB_SW_QCHUNK 4194304u       /* HB_QCHUNK=n: jobs per queue refill in the encode engines (default 256; rounded up to a multiple of 64) */
+#define HB_SW_QCHUNK 4194304u       /* HB_QCHUNK=n: jobs per queue refill in the encode engines (default 256 up to 256-bit primes, 64 above; rounded up to a multiple of 64) */
 uint32_t hb_test_switches(void);
 
 /* Number of visible HIP devices (multi-GPU sharding of encode / prove opens
