@@ -180,9 +180,61 @@ struct HbWmac {
     static constexpr int NG = NL >= 64 ? HB_WMAC_WAVES : HB_WMAC_NG;            // groups of 16 blocks
     static constexpr int NB = 16 * NG;                                          // blocks per workgroup
     static constexpr int TW = (NL / 4 + HB_WMAC_WAVES - 1) / HB_WMAC_WAVES;    // tiles per wave (D <= 4 NL)
-    // LDS: two slice buffers (NB x 64 bytes each), or the limb table (NL x NB x 8 bytes)
-    static constexpr int LDS_BYTES = 2 * NB * 64 > NL * NB * 8 ? 2 * NB * 64 : NL * NB * 8;
+    // LDS: two slice buffers (NB x 64 bytes each), or the limb table (NL x NB x 8 bytes);
+    // then the finish's staging of F and the tags, [NL words][NB blocks] with
+    // a row pitch of NB + 64 / NL words (conflict-free both ways, see below)
+    static constexpr int LIMB_BYTES = 2 * NB * 64 > NL * NB * 8 ? 2 * NB * 64 : NL * NB * 8;
+    // (NL = 64 keeps the per-lane F loads and tag stores: with the staging its
+    // finish spilled more, 12.3 vs 9.0 ms per 8 GiB at 2048 bits, profiles/r06/r6u)
+    static constexpr bool CO = NL <= 32;
+    static constexpr int PITCH = NB + 64 / NL;
+    static constexpr int LDS_BYTES = LIMB_BYTES + (CO ? NL * PITCH * 4 : 0);
 };
+
+// One block's T + F, reduced, out: F from the staging array (co) or from
+// fsrc, the tag into the staging array as big-endian words (co) or to tags.
+template <int NL>
+__device__ __forceinline__ void hb_wmac_finish(const WmacArgs<NL> &A, const long long *lim, u32 *stg, bool co,
+                                               u32 bi, u64 blk) {
+    constexpr int NB = HbWmac<NL>::NB, PITCH = HbWmac<NL>::PITCH;
+    // v = T + F, T = sum_i lim_i 2^(32 i) + kz (limbs past the tiles' digits: kz and the carry)
+    const u32 lt = 4u * A.Mt;
+    const u32 *fp = A.fsrc + blk * NL;
+    u32 v[NL + 1];
+    long long carry = 0;
+    u64 c = 0;
+#pragma unroll
+    for (int t = 0; t < NL; t += 4) {
+        u32 F4[4];
+        if (co) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) F4[k] = stg[(t + k) * PITCH + bi];
+        } else {
+            const uint4 f = *reinterpret_cast<const uint4 *>(fp + t);
+            F4[0] = f.x;
+            F4[1] = f.y;
+            F4[2] = f.z;
+            F4[3] = f.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32 i = (u32)(t + k);
+            const long long xv = (long long)A.kz[i] + (i < lt ? lim[i * NB + bi] : 0ll) + carry;
+            carry = xv >> 32;
+            c += (u64)(u32)xv + F4[k];
+            v[t + k] = (u32)c;
+            c >>= 32;
+        }
+    }
+    v[NL] = (u32)((long long)A.kz[NL] + carry) + (u32)c;
+    hb_reduce_small_lean<NL>(v, A.mod);
+    if (co) {   // word NL - 1 - t of the big-endian tag is limb t
+#pragma unroll
+        for (int t = 0; t < NL; ++t) stg[(NL - 1 - t) * PITCH + bi] = hb_bswap(v[t]);
+    } else {
+        hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, v);
+    }
+}
 
 // WPE: waves per SIMD the register allocator is held to; 0 = the compiler's
 // choice.  The launcher takes HB_WMAC_WPE unless WmacArgs::wpe (test switch
@@ -286,6 +338,28 @@ void hb_wmac_kernel(WmacArgs<NL> A) {
             __syncthreads();
         }
     }
+    // Tags exactly NL words wide (16-byte aligned): the workgroup's F and tags
+    // are contiguous 4 NB NL-byte runs, moved by all threads in coalesced
+    // 16-byte pieces through the staging array -- word w of block b at
+    // stg[w PITCH + b]; a piece (b, q) is words 4 q .. 4 q + 3, and the pitch
+    // puts the 64 lanes of a piece access (64 / (NL / 4) blocks x NL / 4
+    // pieces) and a finish lane's word access on distinct banks.  (One lane
+    // per block reading its 4 NL bytes and writing them back as NL dword
+    // stores 4 NL bytes apart took 1.06 of the kernel's 3.13 ms at 1024 bits:
+    // 64 cache lines per store instruction, profiles/r06/r6t3.)
+    constexpr int PITCH = HbWmac<NL>::PITCH, NQ = NL / 4, NP = NB * NQ, PPT = (NP + NT - 1) / NT;
+    u32 *stg = reinterpret_cast<u32 *>(lds + HbWmac<NL>::LIMB_BYTES);
+    const bool co = HbWmac<NL>::CO && A.tw == 4u * NL && ((uintptr_t)A.tags & 15u) == 0 && ((uintptr_t)A.fsrc & 15u) == 0;
+    const u64 nvalid = A.nfull - w0 < (u64)NB ? A.nfull - w0 : (u64)NB;
+    uint4 fv[PPT];
+    if (co) {   // F in flight while the accumulators go to the limb table
+        const uint4 *fq = reinterpret_cast<const uint4 *>(A.fsrc + w0 * NL);
+#pragma unroll
+        for (int r = 0; r < PPT; ++r) {
+            const u32 u = (u32)r * NT + threadIdx.x;
+            if (u < (u32)NP && u / NQ < nvalid) fv[r] = fq[u];
+        }
+    }
     // the slice buffers are free (every wave passed the last barrier): limb table
     long long *lim = reinterpret_cast<long long *>(lds);
     if (mine) {
@@ -324,34 +398,36 @@ void hb_wmac_kernel(WmacArgs<NL> A) {
             }
         }
     }
-    __syncthreads();
-    if (threadIdx.x >= NB) return;
-    const u32 bi = threadIdx.x;   // block of this lane
-    const u64 blk = w0 + bi;
-    if (blk >= A.nfull) return;
-    // v = T + F, T = sum_i lim_i 2^(32 i) + kz (limbs past the tiles' digits: kz and the carry)
-    const u32 lt = 4u * A.Mt;
-    const u32 *fp = A.fsrc + blk * NL;
-    u32 v[NL + 1];
-    long long carry = 0;
-    u64 c = 0;
+    if (co) {
 #pragma unroll
-    for (int t = 0; t < NL; t += 4) {
-        const uint4 f = *reinterpret_cast<const uint4 *>(fp + t);
-        const u32 F4[4] = {f.x, f.y, f.z, f.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const u32 i = (u32)(t + k);
-            const long long xv = (long long)A.kz[i] + (i < lt ? lim[i * NB + bi] : 0ll) + carry;
-            carry = xv >> 32;
-            c += (u64)(u32)xv + F4[k];
-            v[t + k] = (u32)c;
-            c >>= 32;
+        for (int r = 0; r < PPT; ++r) {
+            const u32 u = (u32)r * NT + threadIdx.x, b = u / NQ, q = u % NQ;
+            if (u < (u32)NP && b < nvalid) {
+                stg[(4 * q) * PITCH + b] = fv[r].x;
+                stg[(4 * q + 1) * PITCH + b] = fv[r].y;
+                stg[(4 * q + 2) * PITCH + b] = fv[r].z;
+                stg[(4 * q + 3) * PITCH + b] = fv[r].w;
+            }
         }
     }
-    v[NL] = (u32)((long long)A.kz[NL] + carry) + (u32)c;
-    hb_reduce_small_lean<NL>(v, A.mod);
-    hb_store_be<NL>(A.tags + blk * (u64)A.tw, A.tw, v);
+    __syncthreads();
+    const u32 bi = threadIdx.x;   // block of this lane
+    if (bi < (u32)NB && bi < nvalid) hb_wmac_finish<NL>(A, lim, stg, co, bi, w0 + bi);
+    if (!co) return;
+    __syncthreads();
+    unsigned char *tq = A.tags + w0 * (u64)(4 * NL);
+#pragma unroll
+    for (int r = 0; r < PPT; ++r) {
+        const u32 u = (u32)r * NT + threadIdx.x, b = u / NQ, q = u % NQ;
+        if (u < (u32)NP && b < nvalid) {
+            uint4 t;
+            t.x = stg[(4 * q) * PITCH + b];
+            t.y = stg[(4 * q + 1) * PITCH + b];
+            t.z = stg[(4 * q + 2) * PITCH + b];
+            t.w = stg[(4 * q + 3) * PITCH + b];
+            *reinterpret_cast<uint4 *>(tq + 16u * u) = t;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ launchers
