@@ -157,7 +157,10 @@ __device__ __forceinline__ void hb_reduce_small_lean(u32 v[NL + 1], const ModP<N
 // fragment once per 16 NG blocks per wave (with the blocks read by every wave
 // straight from global memory and 4 groups, the kernel took 5.7 ms for 8 GiB
 // at 1024 bits, profiles/r06/c; with one wave holding all Mt tiles, 9.0 ms
-// at one wave per SIMD, profiles/r06/b).  Tile t's result at lane (q, n) is
+// at one wave per SIMD, profiles/r06/b).  At NL = 64 (16 tiles) a workgroup
+// is 8 waves x 128 blocks, 2 tiles per wave: half the A-fragment traffic per
+// block of 4 waves x 64 (7.99 vs 8.36 ms per 8 GiB, profiles/r06/r6v).
+// Tile t's result at lane (q, n) is
 // digits 16 t + 4 q .. + 3 of block 16 g + n, i.e. limb 4 t + q; a 4 x 4
 // transpose of (group within a quad of groups, lane row) --
 // v_permlane32_swap, v_permlane16_swap -- leaves lane l with limbs 4 t ..
@@ -168,6 +171,15 @@ __device__ __forceinline__ void hb_reduce_small_lean(u32 v[NL + 1], const ModP<N
 #ifndef HB_WMAC_WAVES
 #define HB_WMAC_WAVES 4
 #endif
+#ifndef HB_WMAC_WPE
+#define HB_WMAC_WPE 3
+#endif
+#ifndef HB_WMAC_WAVES64
+#define HB_WMAC_WAVES64 8
+#endif
+#ifndef HB_WMAC_NG64
+#define HB_WMAC_NG64 8
+#endif
 // K slices in flight from global memory per thread (registers)
 #ifndef HB_WMAC_PF
 #define HB_WMAC_PF 3
@@ -177,9 +189,10 @@ __device__ __forceinline__ void hb_reduce_small_lean(u32 v[NL + 1], const ModP<N
 #endif
 template <int NL>
 struct HbWmac {
-    static constexpr int NG = NL >= 64 ? HB_WMAC_WAVES : HB_WMAC_NG;            // groups of 16 blocks
+    static constexpr int WAVES = NL >= 64 ? HB_WMAC_WAVES64 : HB_WMAC_WAVES;     // waves per workgroup
+    static constexpr int NG = NL >= 64 ? HB_WMAC_NG64 : HB_WMAC_NG;              // groups of 16 blocks
     static constexpr int NB = 16 * NG;                                          // blocks per workgroup
-    static constexpr int TW = (NL / 4 + HB_WMAC_WAVES - 1) / HB_WMAC_WAVES;    // tiles per wave (D <= 4 NL)
+    static constexpr int TW = (NL / 4 + WAVES - 1) / WAVES;                      // tiles per wave (D <= 4 NL)
     // LDS: two slice buffers (NB x 64 bytes each), or the limb table (NL x NB x 8 bytes);
     // then the finish's staging of F and the tags, [NL words][NB blocks] with
     // a row pitch of NB + 64 / NL words (conflict-free both ways, see below)
@@ -189,6 +202,10 @@ struct HbWmac {
     static constexpr bool CO = NL <= 32;
     static constexpr int PITCH = NB + 64 / NL;
     static constexpr int LDS_BYTES = LIMB_BYTES + (CO ? NL * PITCH * 4 : 0);
+    // the default waves-per-SIMD bound: HB_WMAC_WPE; NL = 64 the compiler's
+    // choice (8 waves x 128 blocks: 7.28 ms per 8 GiB at 2048 bits against
+    // 8.1 with WPE 3, whose 168 VGPRs spill 388 bytes; profiles/r06/r6w)
+    static constexpr int WPE = NL >= 64 ? 0 : HB_WMAC_WPE;
 };
 
 // One block's T + F, reduced, out: F from the staging array (co) or from
@@ -239,16 +256,13 @@ __device__ __forceinline__ void hb_wmac_finish(const WmacArgs<NL> &A, const long
 // WPE: waves per SIMD the register allocator is held to; 0 = the compiler's
 // choice.  The launcher takes HB_WMAC_WPE unless WmacArgs::wpe (test switch
 // $HB_WMAC_WPE, A/B) names another instantiated value.
-#ifndef HB_WMAC_WPE
-#define HB_WMAC_WPE 3
-#endif
 template <int WPE>
 struct HbWpe { static constexpr int v = WPE > 0 ? WPE : 1; };
 template <int NL, int WPE>
-__global__ __launch_bounds__(64 * HB_WMAC_WAVES) __attribute__((amdgpu_waves_per_eu(HbWpe<WPE>::v)))
+__global__ __launch_bounds__(64 * HbWmac<NL>::WAVES) __attribute__((amdgpu_waves_per_eu(HbWpe<WPE>::v)))
 void hb_wmac_kernel(WmacArgs<NL> A) {
     constexpr int NG = HbWmac<NL>::NG, NB = HbWmac<NL>::NB, TW = HbWmac<NL>::TW;
-    constexpr int NT = 64 * HB_WMAC_WAVES;
+    constexpr int NT = 64 * HbWmac<NL>::WAVES;
     __shared__ __attribute__((aligned(16))) unsigned char lds[HbWmac<NL>::LDS_BYTES];
     const u32 l = hb_lane_id(), wv = threadIdx.x >> 6;
     const u64 w0 = (u64)blockIdx.x * NB;
@@ -441,16 +455,16 @@ hipError_t hb_launch_wtab(const WtabArgs<NL> &A, hipStream_t s) {
 template <int NL>
 hipError_t hb_launch_wmac(const WmacArgs<NL> &A, hipStream_t s) {
     if (hb_load_only) {
-        hb_load_kernel(&hb_wmac_kernel<NL, HB_WMAC_WPE>);
+        hb_load_kernel(&hb_wmac_kernel<NL, HbWmac<NL>::WPE>);
         return hipSuccess;
     }
     if (A.nfull) {
-        const dim3 g((u32)((A.nfull + HbWmac<NL>::NB - 1) / HbWmac<NL>::NB)), b(64 * HB_WMAC_WAVES);
+        const dim3 g((u32)((A.nfull + HbWmac<NL>::NB - 1) / HbWmac<NL>::NB)), b(64 * HbWmac<NL>::WAVES);
         if (A.wpe == 3) HB_LAUNCH((hb_wmac_kernel<NL, 3>), g, b, s, A);
         else if (A.wpe == 4) HB_LAUNCH((hb_wmac_kernel<NL, 4>), g, b, s, A);
         else if (A.wpe == 5) HB_LAUNCH((hb_wmac_kernel<NL, 5>), g, b, s, A);
         else if (A.wpe == 1) HB_LAUNCH((hb_wmac_kernel<NL, 0>), g, b, s, A);
-        else HB_LAUNCH((hb_wmac_kernel<NL, HB_WMAC_WPE>), g, b, s, A);
+        else HB_LAUNCH((hb_wmac_kernel<NL, HbWmac<NL>::WPE>), g, b, s, A);
     }
     return hipGetLastError();
 }
