@@ -210,3 +210,43 @@ def test_split_cxx_prf_equals_inkernel_mac_and_oracle(nat, oracle, monkeypatch, 
     else:
         for b in sorted(set(np.random.default_rng(3).integers(0, nb, 300).tolist()) | {0, nb - 2, nb - 1}):
             assert got[b] == oracle.cxx_encode(p, S, fk, ak, data[b * C:(b + 1) * C], block_base=b, nblocks=1)[0], b
+
+
+@pytest.mark.parametrize("toff,small", [(16, False), (4, False), (16, True), (4, True)])
+def test_split_tag_alignment(nat, oracle, monkeypatch, toff, small):
+    """hb_wmac_kernel's coalesced finish (F and tags through LDS in 16-byte
+    pieces) runs when the tags are 16-byte aligned, the per-lane finish when
+    they are not (toff = 4: F in a buffer of its own, dword tag stores); both
+    on the two-pass engine and on the mid-size path (F from the quad-PRF
+    launch), with a partial last workgroup (5,001 blocks = 39 x 128 + 9), ==
+    the in-kernel MAC == the oracle."""
+    p = _prime(1024, 777)
+    S, C, w = 10, 1280, 128
+    nbytes = C * 5000 + 77
+    nb = nbytes // C + 1
+    data = np.random.default_rng(toff + 2 * small).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+    fk, ak = hashlib.sha256(b"al-f").digest(), hashlib.sha256(b"al-a").digest()
+    buf = DevBuf(nat, nbytes)
+    res = []
+    try:
+        buf.upload(data)
+        if not small:
+            monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")
+        for no_wide in (False, True):
+            if no_wide:
+                monkeypatch.setenv("HB_NO_WIDE", "1")
+            tb = DevBuf(nat, nb * w + 32)
+            try:
+                tb.upload(b"\xa5" * (nb * w + 32))
+                dev_encode(nat, p, S, fk, ak, buf.p, nbytes, nb, tb.p + toff)
+                raw = tb.download()
+                assert raw[:toff] == b"\xa5" * toff and raw[toff + nb * w:] == b"\xa5" * (32 - toff)
+                res.append(raw[toff:toff + nb * w])
+            finally:
+                tb.free()
+    finally:
+        monkeypatch.delenv("HB_NO_WIDE", raising=False)
+        monkeypatch.delenv("HB_NO_SMALL_ENCODE", raising=False)
+        buf.free()
+    assert res[0] == res[1]
+    assert split_tags(res[0], w) == oracle.encode(p, S, fk, ak, data, nthreads=8)
