@@ -1048,10 +1048,15 @@ int encode_impl(hb_ctx *c, const uint8_t *p_be, size_t p_len, const PrimeInfo &p
     // S = 16 1.2 GiB 3.22 vs 3.72; 2048-bit S = 4 1 GiB 7.20 vs 8.82
     // (profiles/r06/r6j) -- fits of both (mid ~ 4.7 / 2.6 / 6.9 ms per M
     // blocks, two-pass ~ 4.1 / 2.0 / 4.0 ms + 2.8 / 1.3 / 4.6 per M) cross
-    // at 2.2 / 1.6 / 1.7 M blocks, next to the 2.1 M bound below.
+    // at 2.2 / 1.6 / 1.7 M blocks, next to the 2.1 M bound of then.  The
+    // 64-job refills and the coalesced MAC finish sped the two-pass engine up
+    // more: mid vs two-pass 1024-bit 1 GiB 202 vs 200 GiB/s, 1.5 GiB 237 vs
+    // 246, 2 GiB 258 vs 277; 512-bit 1 GiB 334 vs 340, 2 GiB 453 vs 455;
+    // 2048-bit 1 and 2 GiB equal (profiles/r06/r6aa) -- so the bound for
+    // NL >= 16 is now 16 x 256 x #CUs (1 M blocks).
     // $HB_MID_BLOCKS (test switch, A/B): another bound, 0 = none.
     const char *mid_env = sw_env(c, "HB_MID_BLOCKS");
-    const u64 mid_max = mid_env ? strtoull(mid_env, nullptr, 10) : (NL <= 8 ? 17ull : 32ull) * 256ull * (u64)c->num_cus;
+    const u64 mid_max = mid_env ? strtoull(mid_env, nullptr, 10) : (NL <= 8 ? 17ull : 16ull) * 256ull * (u64)c->num_cus;
     const bool small = !cxx && !(flags & HB_ENCODE_SINGLE_PASS) && launch_max &&
                        (use_quad(c, launch_max + S) || launch_max <= mid_max) && !sw_env(c, "HB_NO_SMALL_ENCODE");
     int rc = 0;

@@ -122,7 +122,7 @@ const char *hb_build_flags_string(void);
 #define HB_SW_NO_VERIFY_FUSE 32768u  /* HB_NO_VERIFY_FUSE: verify as a launch sequence (PRFs, mont, hb_wsum_kernel) */
 #define HB_SW_NO_SMALL_ENCODE 65536u /* HB_NO_SMALL_ENCODE: the two-pass engine for small inputs too */
 #define HB_SW_NO_PROVE_UPLOAD 131072u /* HB_NO_PROVE_UPLOAD: small host files are gathered on the host, not uploaded */
-#define HB_SW_MID_BLOCKS 262144u     /* HB_MID_BLOCKS=n: up to n blocks per launch (default 17 x 256 x #CUs; 32 x for primes above 256 bits) take the queued quad-PRF + MAC path */
+#define HB_SW_MID_BLOCKS 262144u     /* HB_MID_BLOCKS=n: up to n blocks per launch (default 17 x 256 x #CUs; 16 x for primes above 256 bits) take the queued quad-PRF + MAC path */
 #define HB_SW_NO_WIDE 524288u       /* HB_NO_WIDE: primes above 256 bits keep the MAC inside the PRF kernels (VALU) instead of the split F-only passes + MFMA MAC (hb_wmac_kernel) */
 #define HB_SW_WMAC_WPE 1048576u     /* HB_WMAC_WPE=1|3|5: hb_wmac_kernel built for another waves-per-SIMD bound (1: the compiler's choice) */
 #define HB_SW_WIDE_SYNC_ALPHA 2097152u /* HB_WIDE_SYNC_ALPHA: the split encode computes alpha and its digit table on the compute stream, before the PRF passes, instead of beside them */

@@ -699,7 +699,7 @@ def test_prove_mixed_residency_equals_device(nat, oracle):
     (256, 16, 65536 * 512),                 # one block more: the quad engine on a job queue
     (256, 1, 32 << 20),                     # 2^20 + 1 blocks: still the queue (17 x 256 x #CUs)
     (256, 1, 36 << 20),                     # 1,179,649 blocks: the two-pass engine
-    (512, 16, 1200 << 20),                  # 1,228,801 blocks of a 512-bit prime: still the queue (32 x)
+    (512, 16, 1000 << 20),                  # 1,024,001 blocks of a 512-bit prime: still the queue (16 x 256 x #CUs)
     (256, 16, (600 << 20) + 5),             # host path: three 256 MiB windows, each on the queue
     (1024, 10, (600 << 20) + 5),            # the same at PySwizzle's defaults (209,715-block windows)
     (256, 1, (3 << 20) + 7),                # S = 1, ragged tail
