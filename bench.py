@@ -504,7 +504,7 @@ def bench_encode(args, cfg, R):
         if not args.no_wide:
             t = time.perf_counter()
             line["wide"] = extra_encode_row(ctx, L, dptr, min(8 * GIB, length), 1024, 10, fk, ak, args,
-                                            steps=5, warmup=2, aes_rate_ref=aes_rate_c3)
+                                            steps=5, warmup=2, aes_rate_ref=aes_rate_c3, with_prove=not args.no_prove)
             line["wide"]["seconds_spent"] = round(time.perf_counter() - t, 1)
         if not args.no_configs1:
             t = time.perf_counter()
@@ -544,7 +544,7 @@ def seeded_prime(bits):
             return x
 
 
-def extra_encode_row(ctx, L, dptr, length, bits, S, fk, ak, args, steps, warmup, aes_rate_ref):
+def extra_encode_row(ctx, L, dptr, length, bits, S, fk, ak, args, steps, warmup, aes_rate_ref, with_prove=False):
     """A device-resident encode of another shape on the first `length` bytes
     of the bench file, tags in a buffer of their own, after the timed region:
     GiB/s over `steps` timed calls, the kernel phases (hb_last_kernel_phases),
@@ -605,8 +605,58 @@ def extra_encode_row(ctx, L, dptr, length, bits, S, fk, ak, args, steps, warmup,
         if not args.no_parity_sample:
             row["parity_sample"] = row_parity(ctx, L, dptr, tptr, length, nblocks, S, p, fk, ak, C, w,
                                               args.parity_blocks)
+        if with_prove:
+            row["prove"] = extra_prove(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, fk, ak,
+                                       check=not args.no_parity_sample)
     finally:
         ctx.check(L.hb_device_free(ctx.h, tptr))
+    return row
+
+
+def extra_prove(ctx, L, dptr, tptr, length, nblocks, S, p, C, w, fk, ak, proofs=50, chunks=10000, check=True):
+    """PySwizzle.prove (PySwizzle.py:333-370) of a 10,000-index challenge
+    (v_max = p) over an extra row's device-resident file and tags, and its
+    verify (PySwizzle.py:372-395, hb_verify_rhs), timed back to back; the
+    proof checked against oracle/swizzle_oracle.c on the challenged blocks
+    and tags copied back."""
+    from heartbeat_amd import _native
+    pb = _native.be(p)
+    ck = hashlib.sha256(b"hb-bench-challenge-wide").digest()
+    mu = ctypes.create_string_buffer(w * S)
+    sg = ctypes.create_string_buffer(w)
+
+    def one():
+        ctx.check(L.hb_prove(ctx.h, pb, len(pb), S, ck, len(ck), chunks, pb, len(pb), tptr, nblocks, dptr, length,
+                             3, mu, sg))
+
+    for _ in range(10):
+        one()
+    t = time.perf_counter()
+    for _ in range(proofs):
+        one()
+    row = {"challenge": "%d indices, v_max = p" % chunks,
+           "ms_per_proof": round((time.perf_counter() - t) / proofs * 1e3, 4), "proofs": proofs,
+           "launches_per_proof": ctx.last_kernel_ms()[1]}
+    row["verify"] = verify_timing(ctx, L, pb, S, fk, ak, nblocks, ck, chunks, mu, sg, proofs)
+    if check:
+        import numpy as np
+        from oracle import oracle as O
+        idx = sorted({O.prf_eval(ck, nblocks, i) for i in range(chunks)})
+        host = np.zeros(length, dtype=np.uint8)          # untouched pages stay unallocated
+        tags = np.zeros(nblocks * w, dtype=np.uint8)
+        for ix in idx:
+            a = ix * C
+            if a < length:
+                ctx.check(L.hb_memcpy(ctx.h, host.ctypes.data + a, dptr.value + a, min(C, length - a), 2))
+            ctx.check(L.hb_memcpy(ctx.h, tags.ctypes.data + ix * w, tptr.value + ix * w, w, 2))
+        ref_mu = ctypes.create_string_buffer(w * S)
+        ref_sg = ctypes.create_string_buffer(w)
+        rc = O.lib().hbo_prove(pb, len(pb), S, ck, len(ck), chunks, pb, len(pb), nblocks,
+                               ctypes.cast(tags.ctypes.data, ctypes.c_char_p), w, host.ctypes.data, length,
+                               ref_mu, ref_sg)
+        if rc:
+            raise RuntimeError("oracle prove error %d" % rc)
+        row["proof_equal_oracle"] = ref_mu.raw == mu.raw and ref_sg.raw == sg.raw
     return row
 
 

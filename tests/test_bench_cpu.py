@@ -54,13 +54,17 @@ def test_default_encode_line_with_every_leg(fake, monkeypatch, capsys, tmp_path)
         r = d[row]
         assert r["parity_sample"]["ok"] is True and r["value"] > 0 and r["aes_per_block"] > 0, row
         assert r["workload"].startswith("%d-bit" % bits) and set(r["phases_ms"]) and r["roofline"]["frac"] > 0
+    wp = d["wide"]["prove"]
+    assert wp["proof_equal_oracle"] is True and wp["verify"]["verified"] is True and wp["ms_per_proof"] > 0
+    assert "prove" not in d["configs1"]
     n = d["config"]["file_bytes_per_rank"]
     assert d["wide"]["blocks"] == n // 1280 + 1 and d["configs1"]["blocks"] == n // 32 + 1
     hp = d["host_path"]
     assert hp["raw_tags_equal"] is True and hp["api_tags_equal"] is True
     assert hp["api_prove_file"]["equal_device_resident_proof"] is True
     for k in ("raw_pageable_gib_s", "raw_register_windows_gib_s", "raw_pinned_gib_s", "api_bytesio_gib_s",
-              "api_bytesio_register_gib_s", "api_file_mmap_gib_s", "api_file_mmap_register_gib_s"):
+              "api_bytesio_register_gib_s", "api_file_mmap_gib_s", "api_file_mmap_register_gib_s",
+              "api_bytesio_register_p1024_s10_gib_s"):
         assert hp[k] > 0, k
     assert set(hp["api_file_mmap_register_phases"]) == {"filebuffer_ms", "encode_ms", "close_ms"}
     assert hp["api_default"]["register_kinds"] == ["mmap", "bytesio", "bytes", "read"]
