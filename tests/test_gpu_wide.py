@@ -250,3 +250,54 @@ def test_split_tag_alignment(nat, oracle, monkeypatch, toff, small):
         buf.free()
     assert res[0] == res[1]
     assert split_tags(res[0], w) == oracle.encode(p, S, fk, ak, data, nthreads=8)
+
+
+@pytest.mark.parametrize("bits,S,nbytes,base", [
+    (1024, 64, 8 << 20, 0),          # 8 KiB blocks: 128 K slices
+    (1024, 250, 8 << 20, 0),         # C = 32,000: the largest column-sum range the int32 MFMA takes
+    (1024, 260, 8 << 20, 0),         # C = 33,280 > 32,768: wide_plan declines, the VALU MAC runs
+    (1024, 10, 4 << 20, 12345),      # a shard's block range (block_base != 0)
+    (512, 1, 8 << 20, 0),            # one 64-byte sector per block: one slice
+    (2048, 1, 4 << 20, 7),           # one 256-byte sector, NL = 64
+])
+@pytest.mark.parametrize("two_pass", [True, False])
+def test_split_shapes_and_block_base(nat, oracle, monkeypatch, bits, S, nbytes, base, two_pass):
+    """More split-encode shapes on both engines (two-pass and the mid-size
+    quad-PRF path): large and single-slice blocks, the C <= 32 KiB bound of
+    the int8 column sums and the fallback past it, and a nonzero block_base
+    (the F PRF's input is block_base + k) == the in-kernel MAC == the oracle
+    (all blocks up to 7,000, else 300 sampled + both ends)."""
+    p = _prime(bits, bits * 7 + S)
+    C = (p.bit_length() // 8) * S
+    nb = nbytes // C + 1
+    w = nat.width_of(p)
+    data = np.random.default_rng(bits + S + base).integers(0, 256, nbytes, dtype=np.uint8).tobytes()
+    fk, ak = hashlib.sha256(b"sb-f%d" % bits).digest(), hashlib.sha256(b"sb-a%d" % bits).digest()
+    buf = DevBuf(nat, nbytes)
+    res = []
+    try:
+        buf.upload(data)
+        if two_pass:
+            monkeypatch.setenv("HB_NO_SMALL_ENCODE", "1")
+        for no_wide in (False, True):
+            if no_wide:
+                monkeypatch.setenv("HB_NO_WIDE", "1")
+            tb = DevBuf(nat, nb * w)
+            try:
+                dev_encode(nat, p, S, fk, ak, buf.p, nbytes, nb, tb.p, block_base=base)
+                res.append(tb.download())
+            finally:
+                tb.free()
+    finally:
+        monkeypatch.delenv("HB_NO_WIDE", raising=False)
+        monkeypatch.delenv("HB_NO_SMALL_ENCODE", raising=False)
+        buf.free()
+    assert res[0] == res[1]
+    got = split_tags(res[0], w)
+    if nb <= 7000:
+        assert got == oracle.encode(p, S, fk, ak, data, block_base=base, nthreads=8)
+    else:
+        rng = np.random.default_rng(nb + base)
+        for b in sorted(set(rng.integers(0, nb, 300).tolist()) | {0, nb - 2, nb - 1}):
+            blk = data[b * C:(b + 1) * C]
+            assert got[b] == oracle.encode(p, S, fk, ak, blk, block_base=base + b, nblocks=1)[0], b
