@@ -496,6 +496,12 @@ struct HbEncodeOcc { static constexpr int v = NL <= 8 ? HB_OCC8 : 1; };
 #ifndef HB_WIDE_WG
 #define HB_WIDE_WG 512
 #endif
+// The F-only passes (ALIGN = 0) of 2048-bit primes hold a 64-limb PRF output
+// per lane: under a 1,024-thread workgroup's 128 VGPRs they spilled 276 bytes
+// per lane; 768 threads (12 waves per CU, 170 VGPRs) is the A/B candidate.
+#ifndef HB_F64_WG
+#define HB_F64_WG 768
+#endif
 #ifndef HB_WIDE_NL
 #define HB_WIDE_NL 32
 #endif
@@ -506,7 +512,7 @@ struct HbEncodeWg { static constexpr int v = NL >= HB_WIDE_NL ? HB_WIDE_WG : HB_
 // workgroups at every prime size -- 16 waves per CU on one LDS table image,
 // the 256-bit kernel's occupancy
 template <int NL, int ALIGN>
-struct HbEncWg { static constexpr int v = ALIGN == 0 ? HB_ENGINE_WG : HbEncodeWg<NL>::v; };
+struct HbEncWg { static constexpr int v = ALIGN == 0 ? (NL >= 64 ? HB_F64_WG : HB_ENGINE_WG) : HbEncodeWg<NL>::v; };
 
 
 __device__ __forceinline__ void hb_zero_sr(u32 sr[4]) { sr[0] = sr[1] = sr[2] = sr[3] = 0; }
