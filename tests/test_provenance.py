@@ -103,7 +103,7 @@ def test_switches_ignored_without_gate(monkeypatch):
     monkeypatch.delenv("HB_ENABLE_TEST_SWITCHES", raising=False)
     for name in ("HB_NO_QUAD", "HB_NO_MFMA", "HB_MFMA_LINE32", "HB_TEST_NO_EARLY_LIST", "HB_TEST_PROVE_BATCH",
                  "HB_MFMA_MIN_S", "HB_TRACE_PHASES", "HB_NO_PROVE_FUSE", "HB_NO_VERIFY_FUSE", "HB_NO_SMALL_ENCODE",
-                 "HB_MID_BLOCKS"):
+                 "HB_MID_BLOCKS", "HB_NO_WIDE", "HB_WMAC_WPE", "HB_WIDE_SYNC_ALPHA", "HB_QCHUNK"):
         monkeypatch.setenv(name, "1")
     assert L.hb_test_switches() == 0
     assert L.hb_build_flags() & _native.HB_BUILD_TEST_SWITCHES == 0
@@ -111,6 +111,7 @@ def test_switches_ignored_without_gate(monkeypatch):
     m = L.hb_test_switches()
     assert m & 1 and m & 2 and m & 8 and m & 32 and m & 128 and m & 16 and m & 256   # HB_SW_* (hbswizzle.h)
     assert m & 8192 and m & 32768 and m & 65536 and m & 262144
+    assert m & 524288 and m & 1048576 and m & 2097152 and m & 4194304   # round 6: wide encode, queue refills
     assert L.hb_build_flags() & _native.HB_BUILD_TEST_SWITCHES
     monkeypatch.setenv("HB_ENABLE_TEST_SWITCHES", "yes")   # only "1" opens the gate
     assert L.hb_test_switches() == 0
